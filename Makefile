@@ -1,0 +1,63 @@
+# Build recipe for librm (HIP, gfx950), the CPU oracle and the headless driver.
+#   make            -> librm.so + oracle + rm_frameloop
+#   make librm      -> opengl-raymarching-in-compute-shader_amd/librm.so
+#   make oracle     -> oracle/_build/librm_oracle.so (test infrastructure)
+#   make goldens    -> oracle/_ref/gen_camera_goldens (needs /root/reference; container only)
+# Built artefacts stay in-tree (git-ignored) so they travel to the GPU box.
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CC       ?= gcc
+CXX      ?= g++
+PKG      := opengl-raymarching-in-compute-shader_amd
+CSRC     := $(PKG)/csrc
+ARCH     ?= gfx950
+# -ffp-contract=off: no FMA contraction (HIP's device default is 'fast'), so every
+# float op is one IEEE op in source order; HIP keeps correctly-rounded f32
+# sqrt/div by default (-fhip-fp32-correctly-rounded-divide-sqrt).
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result
+OFLAGS   := -std=c11 -O2 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall -Wextra
+
+LIBRM    := $(PKG)/librm.so
+ORACLE   := oracle/_build/librm_oracle.so
+DRIVER   := $(PKG)/rm_frameloop
+
+RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_host.cpp
+RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_internal.hpp include/rm_api.h
+
+.PHONY: all librm oracle driver goldens clean
+all: librm oracle driver
+librm: $(LIBRM)
+oracle: $(ORACLE)
+driver: $(DRIVER)
+
+$(PKG)/build/%.o: $(CSRC)/%.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/build/rm_host.o: $(CSRC)/rm_host.cpp $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
+
+$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h
+	@mkdir -p $(dir $@)
+	$(CC) $(OFLAGS) -shared -o $@ oracle/rm_oracle.c -lm
+
+$(DRIVER): $(PKG)/tools/rm_frameloop.cpp include/rm/camera.hpp include/rm/texture.hpp $(LIBRM)
+	$(CXX) -std=c++17 -O2 -Wall -Iinclude -o $@ $< -L$(PKG) -lrm -Wl,-rpath,'$$ORIGIN'
+
+# Camera goldens from the reference's vendored GLM 0.9.8.5 (third-party, in
+# /root/reference/includes/glm).  Output binary only under oracle/_ref/.
+REF ?= /root/reference
+goldens: oracle/_ref/gen_camera_goldens
+	oracle/_ref/gen_camera_goldens > tests/golden/camera_goldens.json
+
+oracle/_ref/gen_camera_goldens: oracle/gen_camera_goldens.cpp
+	@mkdir -p oracle/_ref
+	$(CXX) -std=c++11 -O2 -ffp-contract=off -I$(REF)/includes -o $@ $<
+
+clean:
+	rm -rf $(PKG)/build $(LIBRM) $(DRIVER) oracle/_build oracle/_ref

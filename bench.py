@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X SDF ray marcher (librm).
+
+Metric (BASELINE.json): Mpixels/s = frames/s x W x H of the per-pixel sphere
+tracer (reference hot path shaders/computeShader.glsl, dispatched by
+main.cpp:123), on synthetic frames of the fixed camera sweep S(120) of SURVEY
+8(d).  One "step" = one frame of the sweep rendered by the HIP kernel (for
+N > 1: every rank renders its interleaved row blocks, then an RCCL gather to
+rank 0 and an on-device un-shard assemble the frame).
+
+Default workload = BASELINE config 3: 3840x2160, 3 reflection bounces, soft
+shadows, 4x supersampling, 1 MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..5]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Extra objects:
+  roofline     : FP32-VALU roofline of the dominant kernel (k_wavequeue);
+                 achieved = algorithmic ops per launch (SURVEY 8(d) weights x the
+                 exact work counters of the frames rendered) / mean kernel time
+                 measured with HIP events on the launch stream.
+  cpu_baseline : the CPU oracle (a C restatement of the reference shader) on
+                 this host's cores, on a bounded row sample of the same frame;
+                 its rows are also compared with the GPU frame (parity).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd")
+sys.path.insert(0, PKG)
+
+import rmarch as rm  # noqa: E402
+
+METRIC = "Mpixels/s (frames/s × W×H) at 1/2/4/8 MI355X; max-|Δ| vs GLSL ref"
+
+# BASELINE.json configs (index 1-based as in SURVEY 8(d)).
+CONFIGS = {
+    1: dict(width=512, height=512, bounces=0, aa=False, shadow=rm.RM_SHADOW_HARD,
+            desc="512x512, 0 reflections, hard shadows, no MSAA"),
+    2: dict(width=1920, height=1080, bounces=1, aa=False, shadow=rm.RM_SHADOW_SOFT,
+            desc="1920x1080, 1 reflection, soft shadows, no MSAA"),
+    3: dict(width=3840, height=2160, bounces=3, aa=True, shadow=rm.RM_SHADOW_SOFT,
+            desc="3840x2160, 3 reflections, soft shadows, 4xMSAA"),
+    4: dict(width=3840, height=2160, bounces=5, aa=True, shadow=rm.RM_SHADOW_SOFT,
+            desc="3840x2160, 5 reflections, soft shadows, 4xMSAA"),
+    5: dict(width=7680, height=4320, bounces=3, aa=True, shadow=rm.RM_SHADOW_SOFT,
+            desc="7680x4320, 3 reflections, soft shadows, 4xMSAA"),
+}
+SWEEP_FRAMES = 120
+
+# Algorithmic FP32 ops per unit of work, SURVEY 8(d) (counted as written in the
+# GLSL; uniform-only subexpressions excluded).  See DESIGN.md §6.
+OPS = dict(march=116, reflect=116, shadow=117, normal=446, light=90, ray=33)
+VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # HBM3E spec
+
+
+def algorithmic_ops(c: dict) -> int:
+    return (OPS["march"] * c["march_steps"] + OPS["reflect"] * c["reflect_steps"]
+            + OPS["shadow"] * c["shadow_steps"] + OPS["normal"] * c["normals"]
+            + OPS["light"] * c["lights"] + OPS["ray"] * c["rays"])
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--kernel", default="wavequeue", choices=["wavequeue", "pixel"])
+    ap.add_argument("--row-block", type=int, default=8,
+                    help="rows per interleaved block when sharding over ranks")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-row-stride", type=int, default=4,
+                    help="cpu_baseline renders every k-th row of one frame")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus:
+        if ws == 1 and args.gpus > 1:
+            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run",
+                  file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg["width"], cfg["height"]
+    kernel = rm.RM_KERNEL_WAVEQUEUE if args.kernel == "wavequeue" else rm.RM_KERNEL_PIXEL
+    stream = torch.cuda.current_stream()
+
+    def uniforms(f):
+        return rm.sweep_uniforms(f % SWEEP_FRAMES, SWEEP_FRAMES, cfg["bounces"], cfg["aa"],
+                                 cfg["shadow"])
+
+    if ws > 1:
+        R = args.row_block
+        r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
+                        row_block=R, shard=rank, nshards=ws)
+        rows_cap = r.rows
+        shard_buf = torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(shard_buf.data_ptr())
+        gathered = (torch.empty((ws, rows_cap, W, 4), dtype=torch.uint8, device="cuda")
+                    if rank == 0 else None)
+        frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    else:
+        r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local)
+        frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(frame.data_ptr())
+    r.set_stream(stream.cuda_stream)
+
+    def step(f):
+        r.dispatch(uniforms(f))
+        if ws > 1:
+            glist = list(gathered.unbind(0)) if rank == 0 else None
+            dist.gather(shard_buf, gather_list=glist, dst=0)
+            if rank == 0:
+                r.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
+
+    def barrier():
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- warmup (untimed) ----
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+
+    # ---- timed region: exactly K steps ----
+    r.enable_timing(True)
+    r.kernel_time_ms(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    barrier()
+    t1 = time.perf_counter()
+    kernel_ms, launches = r.kernel_time_ms(reset=True)
+    r.enable_timing(False)
+    elapsed = t1 - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames = args.steps
+    value = frames * W * H / elapsed / 1e6  # whole-job Mpixels/s
+
+    # ---- work counters of exactly the frames timed (untimed pass) ----
+    ops_total = 0
+    cnt_total = None
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, counters=True, device=local,
+                     row_block=args.row_block if ws > 1 else 0, shard=rank if ws > 1 else 0,
+                     nshards=ws) as rc:
+        seen = {}
+        for k in range(args.steps):
+            f = (args.warmup + k) % SWEEP_FRAMES
+            if f not in seen:
+                rc.dispatch(uniforms(f))
+                seen[f] = rc.counters()
+            c = seen[f]
+            ops_total += algorithmic_ops(c)
+            cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
+    mean_kernel_ms = kernel_ms / max(launches, 1)
+    achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
+    bytes_per_launch = r.rows * W * 4
+    hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
+
+    # ---- CPU baseline + parity sample (rank 0, N = 1 only) ----
+    cpu = None
+    parity = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # test/baseline infrastructure only
+        f = (args.warmup + args.steps - 1) % SWEEP_FRAMES
+        u = uniforms(f)
+        rows = list(range(0, H, max(1, args.cpu_row_stride)))
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        c0 = time.perf_counter()
+        ref = O.render(u, W, H, rows=rows, nthreads=threads, want_f32=False, want_counts=False)
+        c1 = time.perf_counter()
+        cpu = {"value": round(len(rows) * W / (c1 - c0) / 1e6, 4), "unit": "Mpixels/s",
+               "cores": threads, "kind": "port",
+               "sample": f"rows py%{args.cpu_row_stride}==0 of sweep frame {f} "
+                         f"({len(rows)}x{W} px, {cfg['desc']}), {c1 - c0:.2f}s wall"}
+        # GPU frame of the same sweep frame: the last step rendered it into `frame`.
+        torch.cuda.synchronize()
+        g = frame.cpu().numpy()[rows]
+        d = np.abs(g.astype(np.int16) - ref["rgba8"].astype(np.int16))
+        parity = {"max_abs_delta_rgba8": int(d.max()), "pixels_over_2": int((d.max(-1) > 2).sum()),
+                  "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / frames * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (camera sweep S(120), SURVEY 8(d))",
+            "config": {"workload": f"cfg{args.config}: {cfg['desc']}", "width": W, "height": H,
+                       "bounces": cfg["bounces"], "aa": cfg["aa"],
+                       "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
+                       "kernel": f"k_{args.kernel}",
+                       "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
+                                       if ws > 1 else "single GPU")},
+            "fps": round(frames / elapsed, 3),
+            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3),
+                         "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
+                         "traffic": None,
+                         "kernel": f"k_{args.kernel}", "mean_kernel_ms": round(mean_kernel_ms, 4),
+                         "ops_per_launch": int(ops_total / max(launches, 1)),
+                         "hbm_write_GBs": round(hbm_gbs, 2),
+                         "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
+            "work": cnt_total,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    r.close()
+    if ws > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

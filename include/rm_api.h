@@ -1,0 +1,230 @@
+/*
+ * rm_api.h — C-ABI of librm, the MI355X-native SDF ray marcher.
+ *
+ * This is the drop-in boundary that replaces the reference's GL compute
+ * program + dispatch (Qirias/OpenGL-RayMarching-in-Compute-Shader):
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  ------------------------------------
+ *   CreateCompute            shader.hpp:186-197  rm_create (kernels are compiled AOT)
+ *   setBool/setInt/setuInt/  shader.hpp:19-69    rm_set_bool/int/uint/float/vec2/3/4
+ *   setFloat/setVec2/3/4     (called by name from main.cpp:99-120)
+ *   glDispatchCompute        main.cpp:123        rm_dispatch (async, on the ctx stream)
+ *   glMemoryBarrier          main.cpp:125        rm_synchronize
+ *   Texture::GenerateTexture texture.cpp:10-21   device image owned by rm_ctx
+ *   (no readback in the ref; quad draw only)     rm_read_rgba8 / rm_read_rgba32f
+ *   Camera ctor/setMouse/lookAt camera.cpp:8-51  rm_camera_* (glm-free, same formulas)
+ *
+ * Conventions: every entry point returns 0 (RM_OK) on success and a negative
+ * RM_ERR_* on failure, with a message available from rm_last_error(ctx).  The
+ * one non-error positive code is RM_WARN_UNKNOWN_UNIFORM: like GL's location
+ * -1 (shader.hpp:21 glUniform*(-1, ...) is a silent no-op) an unknown uniform
+ * name changes nothing, but the caller can see that it happened.
+ * No C++ exception crosses this boundary.  One context per host thread (the
+ * same constraint as the reference's thread-bound GL context, main.cpp:59).
+ * The context owns its device buffers and stream; the caller owns host buffers.
+ */
+#ifndef RM_API_H
+#define RM_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RM_API_VERSION 1
+
+/* ---- status codes --------------------------------------------------------- */
+#define RM_OK 0
+#define RM_WARN_UNKNOWN_UNIFORM 1 /* name not in the uniform block: no-op */
+#define RM_ERR_INVALID (-1)       /* bad argument / shape */
+#define RM_ERR_HIP (-2)           /* HIP runtime error */
+#define RM_ERR_NOMEM (-3)         /* device or host allocation failed */
+#define RM_ERR_NO_DEVICE (-4)     /* no HIP device (librm never falls back to CPU) */
+#define RM_ERR_STATE (-5)         /* call not valid in this state */
+
+/* ---- output image formats (bitmask for rm_config.outputs) ----------------- */
+#define RM_OUT_RGBA8 1   /* display format (what the quad shows, Quad.glsl:21-25) */
+#define RM_OUT_RGBA32F 2 /* the reference texture's true storage (texture.cpp:19) */
+
+/* ---- shadow modes (rm_uniforms.shadow_mode) ------------------------------- */
+#define RM_SHADOW_SOFT 0 /* reference: softshadow(k = 2.0)  computeShader.glsl:185,236 */
+#define RM_SHADOW_HARD 1 /* extension: k = +inf -> shadow in {0.05, 1}  (BASELINE cfg 1) */
+
+/* ---- kernel variants (rm_config.kernel) ----------------------------------- */
+#define RM_KERNEL_AUTO 0       /* = RM_KERNEL_WAVEQUEUE */
+#define RM_KERNEL_PIXEL 1      /* one thread per pixel, structured control flow */
+#define RM_KERNEL_WAVEQUEUE 2  /* persistent waves, per-lane job refill (ballot/popc) */
+
+/* Uniform block of computeShader.glsl:7,59-66.  vec4s carry w = 0
+ * (main.cpp:103-106).  Layout is plain C, not std140. */
+typedef struct rm_camera {
+  float pos[4];   /* camera.pos    glsl:16 */
+  float dir[4];   /* camera.dir    glsl:17 (forward) */
+  float yAxis[4]; /* camera.yAxis  glsl:18 (up) */
+  float xAxis[4]; /* camera.xAxis  glsl:19 (right) */
+} rm_camera;
+
+typedef struct rm_light { /* glsl:22-32 */
+  float position[3];
+  float ambient[3];
+  float diffuse[3];
+  float specular[3];
+  float constant;
+  float linear;
+  float quadratic;
+} rm_light;
+
+typedef struct rm_uniforms {
+  rm_camera camera;     /* glsl:65 */
+  rm_light light;       /* glsl:66 */
+  float iTime;          /* glsl:62  drives the box/sphere blend, sin(iTime)/2+0.5 (glsl:117) */
+  int32_t bounceVar;    /* glsl:60  0..5 (main.cpp:199-204) */
+  int32_t AA;           /* glsl:59  4x supersampling on/off */
+  uint32_t workgroups;  /* glsl:7   launch geometry only; ignored (librm picks its own) */
+  float drand48;        /* glsl:61  unused by the shader; accepted and ignored */
+  float mouse[3];       /* glsl:63  unused by the shader; accepted and ignored */
+  float iMouse[2];      /* glsl:64  unused by the shader; accepted and ignored */
+  int32_t shadow_mode;  /* extension: RM_SHADOW_SOFT (reference) or RM_SHADOW_HARD */
+} rm_uniforms;
+
+/* Work counters, in the reference's units (calls as written in the GLSL). */
+typedef struct rm_counters {
+  uint64_t rays;          /* castRay calls                       glsl:68 */
+  uint64_t march_steps;   /* sdf() calls inside RayMarch         glsl:131-139 */
+  uint64_t reflect_steps; /* sdf() calls inside reflectedRay     glsl:150-158 */
+  uint64_t shadow_steps;  /* sdf() calls inside softshadow       glsl:205-213 */
+  uint64_t normals;       /* GetNormal calls (4 sdf each)        glsl:278-288 */
+  uint64_t lights;        /* getPointLight calls                 glsl:253-276 */
+  uint64_t sdf_evals;     /* march + reflect + shadow + 4*normals */
+} rm_counters;
+
+typedef struct rm_config {
+  int32_t width;      /* image width  (SCREEN_WIDTH,  main.cpp:16) */
+  int32_t height;     /* image height (SCREEN_HEIGHT, main.cpp:17) */
+  int32_t device;     /* HIP device ordinal; -1 = current device */
+  int32_t outputs;    /* RM_OUT_* bitmask; 0 = RM_OUT_RGBA8 */
+  int32_t kernel;     /* RM_KERNEL_*; 0 = auto */
+  int32_t counters;   /* nonzero: collect rm_counters + per-pixel sdf counts (slower) */
+  /* Row sharding (multi-GPU): the image's rows are cut into
+   * blocks of row_block rows; block b belongs to shard b % nshards.  This
+   * context renders only shard `shard`'s rows, packed in block order, into a
+   * [rows_cap][width] image (rows_cap = rm_shard_rows_cap()).  nshards <= 1
+   * means the whole image. */
+  int32_t row_block;
+  int32_t shard;
+  int32_t nshards;
+} rm_config;
+
+typedef struct rm_ctx rm_ctx;
+
+/* ---- lifetime ------------------------------------------------------------- */
+int rm_create(rm_ctx **out, const rm_config *cfg);
+void rm_destroy(rm_ctx *ctx);
+const char *rm_last_error(const rm_ctx *ctx);
+int rm_api_version(void);
+int rm_device_count(int *count);
+
+/* ---- uniforms: by-name setters mirroring shader.hpp:19-69 ------------------
+ * Names are the GLSL ones: "iTime", "workgroups", "AA", "bounceVar",
+ * "drand48", "mouse", "iMouse", "camera.pos", "camera.dir", "camera.yAxis",
+ * "camera.xAxis", "light.position", "light.ambient", "light.diffuse",
+ * "light.specular", "light.constant", "light.linear", "light.quadratic",
+ * plus the extension "shadow_mode". */
+int rm_set_bool(rm_ctx *ctx, const char *name, int value);
+int rm_set_int(rm_ctx *ctx, const char *name, int32_t value);
+int rm_set_uint(rm_ctx *ctx, const char *name, const uint32_t *value);
+int rm_set_float(rm_ctx *ctx, const char *name, float value);
+int rm_set_vec2(rm_ctx *ctx, const char *name, float x, float y);
+int rm_set_vec3(rm_ctx *ctx, const char *name, float x, float y, float z);
+int rm_set_vec4(rm_ctx *ctx, const char *name, float x, float y, float z, float w);
+int rm_set_uniforms(rm_ctx *ctx, const rm_uniforms *u);
+int rm_get_uniforms(const rm_ctx *ctx, rm_uniforms *u);
+
+/* Defaults of main.cpp:100-120 for the lights/flags and the reference's
+ * start-up camera (pos 0, looking down -z): AA on, bounceVar 0, soft shadow. */
+int rm_default_uniforms(rm_uniforms *u);
+
+/* ---- dispatch / barrier / readback --------------------------------------- */
+/* Render one frame with the current uniforms. Asynchronous on the context's
+ * stream (== glDispatchCompute, main.cpp:123). */
+int rm_dispatch(rm_ctx *ctx);
+/* Wait for all work queued on the context (== glMemoryBarrier + the
+ * implicit sync of the draw, main.cpp:125-134). */
+int rm_synchronize(rm_ctx *ctx);
+/* Synchronous readback. Row 0 of the image is the bottom row (py = 0,
+ * quad.hpp:9); flip_y != 0 writes the top row first (image-file order).
+ * row_pitch is in bytes; 0 = tightly packed. For a sharded context the
+ * packed [rows_cap][width] shard image is read (flip_y must be 0). */
+int rm_read_rgba8(rm_ctx *ctx, uint8_t *dst, size_t row_pitch, int flip_y);
+int rm_read_rgba32f(rm_ctx *ctx, float *dst, size_t row_pitch, int flip_y);
+/* Counters of the last dispatch (requires cfg.counters). */
+int rm_get_counters(rm_ctx *ctx, rm_counters *out);
+/* Per-pixel sdf() evaluation counts of the last dispatch, summed over the
+ * pixel's samples, reference units (requires cfg.counters). */
+int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
+
+/* ---- device-side interop (plain pointers; for stream/collective plumbing) - */
+/* Use an external stream (hipStream_t passed as void*); NULL = own stream. */
+int rm_set_stream(rm_ctx *ctx, void *hip_stream);
+/* Render RGBA8 into a caller-owned device buffer of >= rows*width*4 bytes
+ * (rows = height, or rows_cap when sharded) instead of the context's own.
+ * NULL restores the internal buffer. */
+int rm_set_output_rgba8(rm_ctx *ctx, void *device_ptr);
+/* Device pointer of the RGBA8 image the next dispatch writes. */
+int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
+/* Assemble a full image from nshards packed shard images laid out
+ * back-to-back ([nshards][rows_cap][width] RGBA8, e.g. the result of an RCCL
+ * gather) into `frame` ([height][width] RGBA8), both device pointers, on the
+ * context's stream. Uses the context's width/height/row_block/nshards. */
+int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
+/* Kernel timing: when enabled, HIP events bracket every render-kernel launch
+ * on the launch stream; rm_kernel_time_ms returns the summed kernel time and
+ * launch count since the last reset (synchronizes). */
+int rm_enable_timing(rm_ctx *ctx, int enable);
+int rm_kernel_time_ms(rm_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+/* ---- row sharding helpers (pure functions) ------------------------------- */
+int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);
+/* Global row (py) of local row `local_row` of shard `shard`; -1 if padding. */
+int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
+                            int32_t local_row);
+
+/* ---- Camera (source/camera.{hpp,cpp}), glm-free, same formulas ----------- */
+typedef struct rm_camera_state { /* members of camera.hpp:14-27 */
+  int32_t width, height;
+  float angleY, angleX;
+  float mouseSensitivity, keyboardSpeed;
+  float xpos, ypos;
+  float cameraPos[3];
+  float forward[3];
+  float up[3];
+  float right[3];
+} rm_camera_state;
+
+/* Camera::Camera(w,h,sens,speed,pos,lookAt,up)  camera.cpp:8-14 */
+int rm_camera_init(rm_camera_state *c, int32_t width, int32_t height, float mouseSensitivity,
+                   float keyboardSpeed, const float pos[3], const float lookAt[3],
+                   const float up[3]);
+/* Camera::setMouse                              camera.cpp:16-20 */
+int rm_camera_set_mouse(rm_camera_state *c, float x, float y);
+/* Camera::lookAt                                camera.cpp:22-51 */
+int rm_camera_look_at(rm_camera_state *c, int zN, int zP, int xN, int xP, int halfSpeed,
+                      float deltaTime);
+/* The four setVec4 calls of main.cpp:103-106 (w = 0). */
+int rm_camera_to_uniform(const rm_camera_state *c, rm_camera *out);
+
+/* ---- synthetic frames -------------------------------------- */
+/* Sweep S(F): camera at (0,0,15), yaw -20..+20 deg over F frames, pitch -5 deg,
+ * iTime = f/60; lights of main.cpp:108-114. frame < 0 selects the default
+ * frame D (start-up view: pos 0, yaw = pitch = 0, iTime = 0). */
+int rm_sweep_uniforms(int32_t frame, int32_t nframes, int32_t bounceVar, int32_t AA,
+                      int32_t shadow_mode, rm_uniforms *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RM_API_H */

@@ -1,0 +1,485 @@
+// rm_api.hip — librm's C-ABI: context, uniforms, dispatch, readback, timing.
+//
+// Replaces the reference's GL program + dispatch (see include/rm_api.h for the
+// call-by-call mapping).  There is no CPU backend: without a HIP device
+// rm_create fails with RM_ERR_NO_DEVICE — librm never falls back to the CPU.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "rm_internal.hpp"
+#include "rm_scene.hpp"
+
+namespace rm {
+hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
+hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
+hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
+                          int nshards, int rows_cap, hipStream_t s);
+}  // namespace rm
+
+struct rm_ctx {
+  rm_config cfg{};
+  int device = 0;
+  int rows = 0;  // rows rendered per dispatch (height, or the shard's rows_cap)
+  int num_cus = 256;
+  rm_uniforms u{};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  uint8_t* d_rgba8 = nullptr;     // own RGBA8 image
+  uint8_t* ext_rgba8 = nullptr;   // caller-provided RGBA8 image (rm_set_output_rgba8)
+  float* d_rgba32f = nullptr;
+  uint32_t* d_counts = nullptr;
+  unsigned long long* d_counters = nullptr;
+  uint32_t* d_queue = nullptr;
+  bool dispatched = false;
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
+  double total_ms = 0.0;
+  int64_t launches = 0;
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+int fail(rm_ctx* c, int code, const std::string& msg) {
+  if (c)
+    c->err = msg;
+  else
+    g_create_error = msg;
+  return code;
+}
+
+int hip_fail(rm_ctx* c, hipError_t e, const char* what) {
+  return fail(c, RM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RM_HIP(c, call)                              \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
+  } while (0)
+
+int set_device(rm_ctx* c) {
+  RM_HIP(c, hipSetDevice(c->device));
+  return RM_OK;
+}
+
+rmd::Frame make_frame(const rm_ctx* c) {
+  const rm_uniforms& u = c->u;
+  rmd::Frame F;
+  std::memset(&F, 0, sizeof F);
+  std::memcpy(F.cam_pos, u.camera.pos, sizeof F.cam_pos);
+  std::memcpy(F.cam_dir, u.camera.dir, sizeof F.cam_dir);
+  std::memcpy(F.cam_y, u.camera.yAxis, sizeof F.cam_y);
+  std::memcpy(F.cam_x, u.camera.xAxis, sizeof F.cam_x);
+  std::memcpy(F.lpos, u.light.position, sizeof F.lpos);
+  std::memcpy(F.lamb, u.light.ambient, sizeof F.lamb);
+  std::memcpy(F.ldif, u.light.diffuse, sizeof F.ldif);
+  std::memcpy(F.lspec, u.light.specular, sizeof F.lspec);
+  F.lconst = u.light.constant;
+  F.llin = u.light.linear;
+  F.lquad = u.light.quadratic;
+  // Uniform-only subexpressions, evaluated once on the host with the same
+  // float operations the GLSL performs per call (glsl:70, 117, 185/236).
+  F.blend = std::sin(u.iTime) / 2.0f + 0.5f;
+  F.omblend = 1.0f - F.blend;
+  F.k = (u.shadow_mode == RM_SHADOW_HARD) ? INFINITY : 2.0f;
+  F.persp = 45.0f * static_cast<float>(0.01745329251994329576923690768489);
+  F.bounces = u.bounceVar;
+  F.aa = u.AA ? 1 : 0;
+  F.width = c->cfg.width;
+  F.height = c->cfg.height;
+  F.row_block = c->cfg.row_block;
+  F.shard = c->cfg.shard;
+  F.nshards = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
+  F.rows = c->rows;
+  F.rgba8 = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
+  F.rgba32f = (c->cfg.outputs & RM_OUT_RGBA32F) ? c->d_rgba32f : nullptr;
+  F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
+  F.counters = c->cfg.counters ? c->d_counters : nullptr;
+  F.queue = c->d_queue;
+  return F;
+}
+
+void free_all(rm_ctx* c) {
+  if (c->d_rgba8) (void)hipFree(c->d_rgba8);
+  if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
+  if (c->d_counts) (void)hipFree(c->d_counts);
+  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_queue) (void)hipFree(c->d_queue);
+  for (auto& p : c->ev_pool) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  c->ev_pool.clear();
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  c->d_rgba8 = nullptr;
+  c->d_rgba32f = nullptr;
+  c->d_counts = nullptr;
+  c->d_counters = nullptr;
+  c->d_queue = nullptr;
+  c->stream = nullptr;
+}
+
+int check_uniforms(rm_ctx* c, const rm_uniforms& u) {
+  if (u.bounceVar < 0 || u.bounceVar > 5)
+    return fail(c, RM_ERR_INVALID, "bounceVar must be in 0..5 (main.cpp:199-204)");
+  if (u.shadow_mode != RM_SHADOW_SOFT && u.shadow_mode != RM_SHADOW_HARD)
+    return fail(c, RM_ERR_INVALID, "shadow_mode must be RM_SHADOW_SOFT or RM_SHADOW_HARD");
+  return RM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rm_last_error(const rm_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int rm_device_count(int* count) {
+  if (!count) return RM_ERR_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = (e == hipSuccess) ? n : 0;
+  return RM_OK;
+}
+
+int rm_create(rm_ctx** out, const rm_config* cfg) {
+  if (!out || !cfg) return fail(nullptr, RM_ERR_INVALID, "rm_create: null argument");
+  *out = nullptr;
+  if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65536 || cfg->height > 65536)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: width/height must be in 1..65536");
+  if (cfg->outputs & ~(RM_OUT_RGBA8 | RM_OUT_RGBA32F))
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown output bits");
+  if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_WAVEQUEUE)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
+  if (cfg->nshards > 1 &&
+      (cfg->row_block <= 0 || cfg->shard < 0 || cfg->shard >= cfg->nshards))
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: bad row_block/shard/nshards");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, RM_ERR_NO_DEVICE,
+                "rm_create: no HIP device (librm has no CPU fallback; use a GPU box)");
+  rm_ctx* c = new (std::nothrow) rm_ctx();
+  if (!c) return fail(nullptr, RM_ERR_NOMEM, "rm_create: out of host memory");
+  c->cfg = *cfg;
+  if (c->cfg.outputs == 0) c->cfg.outputs = RM_OUT_RGBA8;
+  if (c->cfg.nshards <= 1) {
+    c->cfg.nshards = 1;
+    c->cfg.shard = 0;
+    if (c->cfg.row_block <= 0) c->cfg.row_block = 1;
+  }
+  if (cfg->device >= 0) {
+    c->device = cfg->device;
+  } else {
+    if (hipGetDevice(&c->device) != hipSuccess) c->device = 0;
+  }
+  if (c->device >= ndev) {
+    delete c;
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: device ordinal out of range");
+  }
+  int rc = RM_OK;
+  auto bail = [&](int code) {
+    g_create_error = c->err;
+    free_all(c);
+    delete c;
+    return code;
+  };
+  if ((rc = set_device(c)) != RM_OK) return bail(rc);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cus = prop.multiProcessorCount;
+  rm_shard_rows_cap(c->cfg.height, c->cfg.row_block, c->cfg.nshards, &c->rows);
+  const size_t npx = (size_t)c->rows * (size_t)c->cfg.width;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return bail(hip_fail(c, e, "hipStreamCreate"));
+  c->own_stream = true;
+  if (c->cfg.outputs & RM_OUT_RGBA8) {
+    if ((e = hipMalloc(&c->d_rgba8, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc rgba8"));
+    if ((e = hipMemset(c->d_rgba8, 0, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
+  }
+  if (c->cfg.outputs & RM_OUT_RGBA32F) {
+    if ((e = hipMalloc(&c->d_rgba32f, npx * 16)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc rgba32f"));
+    if ((e = hipMemset(c->d_rgba32f, 0, npx * 16)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
+  }
+  if (c->cfg.counters) {
+    if ((e = hipMalloc(&c->d_counts, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc counts"));
+    if ((e = hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess)
+      return bail(hip_fail(c, e, "hipMalloc counters"));
+  }
+  if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
+  rm_default_uniforms(&c->u);
+  *out = c;
+  return RM_OK;
+}
+
+void rm_destroy(rm_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  free_all(ctx);
+  delete ctx;
+}
+
+// ---- uniforms -------------------------------------------------------------------
+static int set_floats(rm_ctx* c, const char* name, const float* v, int n) {
+  if (!c || !name) return RM_ERR_INVALID;
+  int m = 0;
+  float* dst = rm::uniform_floats(&c->u, name, &m);
+  if (!dst) return RM_WARN_UNKNOWN_UNIFORM;
+  // glUniform with a mismatched component count is a GL error that leaves the
+  // uniform unchanged; report it instead of writing.
+  if (m != n) return fail(c, RM_ERR_INVALID, std::string("uniform '") + name + "' has " +
+                                                 std::to_string(m) + " components");
+  std::memcpy(dst, v, sizeof(float) * n);
+  return RM_OK;
+}
+
+static int set_int(rm_ctx* c, const char* name, int32_t v) {
+  if (!c || !name) return RM_ERR_INVALID;
+  int32_t* dst = rm::uniform_ints(&c->u, name);
+  if (!dst) {
+    int m = 0;
+    if (rm::uniform_floats(&c->u, name, &m))
+      return fail(c, RM_ERR_INVALID, std::string("uniform '") + name + "' is a float");
+    return RM_WARN_UNKNOWN_UNIFORM;
+  }
+  rm_uniforms t = c->u;
+  *rm::uniform_ints(&t, name) = v;
+  int rc = check_uniforms(c, t);
+  if (rc != RM_OK) return rc;
+  *dst = v;
+  return RM_OK;
+}
+
+int rm_set_bool(rm_ctx* c, const char* name, int value) { return set_int(c, name, value ? 1 : 0); }
+int rm_set_int(rm_ctx* c, const char* name, int32_t value) { return set_int(c, name, value); }
+int rm_set_uint(rm_ctx* c, const char* name, const uint32_t* value) {
+  if (!value) return RM_ERR_INVALID;
+  return set_int(c, name, (int32_t)*value);
+}
+int rm_set_float(rm_ctx* c, const char* name, float value) { return set_floats(c, name, &value, 1); }
+int rm_set_vec2(rm_ctx* c, const char* name, float x, float y) {
+  const float v[2] = {x, y};
+  return set_floats(c, name, v, 2);
+}
+int rm_set_vec3(rm_ctx* c, const char* name, float x, float y, float z) {
+  const float v[3] = {x, y, z};
+  return set_floats(c, name, v, 3);
+}
+int rm_set_vec4(rm_ctx* c, const char* name, float x, float y, float z, float w) {
+  const float v[4] = {x, y, z, w};
+  return set_floats(c, name, v, 4);
+}
+
+int rm_set_uniforms(rm_ctx* c, const rm_uniforms* u) {
+  if (!c || !u) return RM_ERR_INVALID;
+  int rc = check_uniforms(c, *u);
+  if (rc != RM_OK) return rc;
+  c->u = *u;
+  return RM_OK;
+}
+
+int rm_get_uniforms(const rm_ctx* c, rm_uniforms* u) {
+  if (!c || !u) return RM_ERR_INVALID;
+  *u = c->u;
+  return RM_OK;
+}
+
+// ---- dispatch ---------------------------------------------------------------------
+int rm_dispatch(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if (c->cfg.counters) {
+    RM_HIP(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+  }
+  rmd::Frame F = make_frame(c);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    if (c->ev_used == c->ev_pool.size()) {
+      std::pair<hipEvent_t, hipEvent_t> p;
+      RM_HIP(c, hipEventCreate(&p.first));
+      RM_HIP(c, hipEventCreate(&p.second));
+      c->ev_pool.push_back(p);
+    }
+    e0 = c->ev_pool[c->ev_used].first;
+    e1 = c->ev_pool[c->ev_used].second;
+    c->ev_used++;
+  }
+  const int kernel = c->cfg.kernel == RM_KERNEL_AUTO ? RM_KERNEL_WAVEQUEUE : c->cfg.kernel;
+  if (kernel == RM_KERNEL_WAVEQUEUE) {
+    RM_HIP(c, hipMemsetAsync(c->d_queue, 0, 256, c->stream));
+  }
+  if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
+  hipError_t e = (kernel == RM_KERNEL_PIXEL)
+                     ? rm::launch_pixel(F, c->cfg.counters != 0, c->stream)
+                     : rm::launch_wavequeue(F, c->cfg.counters != 0, c->stream, c->num_cus);
+  if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+  if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
+  c->dispatched = true;
+  return RM_OK;
+}
+
+int rm_synchronize(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  return RM_OK;
+}
+
+static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t row_pitch,
+                      int flip_y) {
+  if (!c || !dst) return RM_ERR_INVALID;
+  if (!dev) return fail(c, RM_ERR_STATE, "output format not enabled in rm_config.outputs");
+  if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
+  if (flip_y && c->cfg.nshards > 1)
+    return fail(c, RM_ERR_INVALID, "flip_y is not defined for a packed shard image");
+  const size_t w = (size_t)c->cfg.width * bpp;
+  if (row_pitch == 0) row_pitch = w;
+  if (row_pitch < w) return fail(c, RM_ERR_INVALID, "row_pitch smaller than a row");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  const size_t rows = (size_t)c->rows;
+  RM_HIP(c, hipMemcpy2D(dst, row_pitch, dev, w, w, rows, hipMemcpyDeviceToHost));
+  if (flip_y) {
+    // Row 0 of the device image is the bottom row (quad.hpp:9); flip in place
+    // so the top row comes first (image-file order).
+    std::vector<char> tmp(w);
+    char* base = static_cast<char*>(dst);
+    for (size_t r = 0; r < rows / 2; ++r) {
+      char* a = base + r * row_pitch;
+      char* b = base + (rows - 1 - r) * row_pitch;
+      std::memcpy(tmp.data(), a, w);
+      std::memcpy(a, b, w);
+      std::memcpy(b, tmp.data(), w);
+    }
+  }
+  return RM_OK;
+}
+
+int rm_read_rgba8(rm_ctx* c, uint8_t* dst, size_t row_pitch, int flip_y) {
+  if (!c) return RM_ERR_INVALID;
+  const void* dev = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
+  return read_image(c, dev, 4, dst, row_pitch, flip_y);
+}
+
+int rm_read_rgba32f(rm_ctx* c, float* dst, size_t row_pitch, int flip_y) {
+  if (!c) return RM_ERR_INVALID;
+  return read_image(c, c->d_rgba32f, 16, dst, row_pitch, flip_y);
+}
+
+int rm_get_counters(rm_ctx* c, rm_counters* out) {
+  if (!c || !out) return RM_ERR_INVALID;
+  if (!c->cfg.counters) return fail(c, RM_ERR_STATE, "context created without counters");
+  if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  unsigned long long h[8];
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  RM_HIP(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+  out->rays = h[0];
+  out->march_steps = h[1];
+  out->reflect_steps = h[2];
+  out->shadow_steps = h[3];
+  out->normals = h[4];
+  out->lights = h[5];
+  out->sdf_evals = h[1] + h[2] + h[3] + 4 * h[4];
+  return RM_OK;
+}
+
+int rm_read_sdf_counts(rm_ctx* c, uint32_t* dst) {
+  if (!c || !dst) return RM_ERR_INVALID;
+  if (!c->cfg.counters) return fail(c, RM_ERR_STATE, "context created without counters");
+  if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  RM_HIP(c, hipMemcpy(dst, c->d_counts, (size_t)c->rows * c->cfg.width * 4, hipMemcpyDeviceToHost));
+  return RM_OK;
+}
+
+// ---- device interop ----------------------------------------------------------------
+int rm_set_stream(rm_ctx* c, void* hip_stream) {
+  if (!c) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if (c->own_stream && c->stream) {
+    RM_HIP(c, hipStreamSynchronize(c->stream));
+    (void)hipStreamDestroy(c->stream);
+    c->stream = nullptr;
+    c->own_stream = false;
+  }
+  if (hip_stream) {
+    c->stream = static_cast<hipStream_t>(hip_stream);
+  } else {
+    RM_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return RM_OK;
+}
+
+int rm_set_output_rgba8(rm_ctx* c, void* device_ptr) {
+  if (!c) return RM_ERR_INVALID;
+  if (!(c->cfg.outputs & RM_OUT_RGBA8))
+    return fail(c, RM_ERR_STATE, "RGBA8 output not enabled in rm_config.outputs");
+  c->ext_rgba8 = static_cast<uint8_t*>(device_ptr);
+  return RM_OK;
+}
+
+int rm_get_output_rgba8(rm_ctx* c, void** device_ptr) {
+  if (!c || !device_ptr) return RM_ERR_INVALID;
+  *device_ptr = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
+  return RM_OK;
+}
+
+int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
+  if (!c || !gathered_dev || !frame_dev) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  hipError_t e = rm::launch_unshard(gathered_dev, frame_dev, c->cfg.width, c->cfg.height,
+                                    c->cfg.row_block, c->cfg.nshards, c->rows, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
+  return RM_OK;
+}
+
+int rm_enable_timing(rm_ctx* c, int enable) {
+  if (!c) return RM_ERR_INVALID;
+  c->timing = enable != 0;
+  return RM_OK;
+}
+
+int rm_kernel_time_ms(rm_ctx* c, double* total_ms, int64_t* launches, int reset) {
+  if (!c) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  for (size_t i = 0; i < c->ev_used; ++i) {
+    RM_HIP(c, hipEventSynchronize(c->ev_pool[i].second));
+    float ms = 0.0f;
+    RM_HIP(c, hipEventElapsedTime(&ms, c->ev_pool[i].first, c->ev_pool[i].second));
+    c->total_ms += ms;
+    c->launches++;
+  }
+  c->ev_used = 0;
+  if (total_ms) *total_ms = c->total_ms;
+  if (launches) *launches = c->launches;
+  if (reset) {
+    c->total_ms = 0.0;
+    c->launches = 0;
+  }
+  return RM_OK;
+}
+
+}  // extern "C"

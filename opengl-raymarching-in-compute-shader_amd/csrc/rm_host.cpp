@@ -1,0 +1,314 @@
+// rm_host.cpp — host-side pieces of librm that need no GPU:
+//   * Camera (source/camera.{hpp,cpp}) restated without GLM/GLFW, reproducing
+//     GLM 0.9.8.5's operation order so the basis is bit-identical to what the
+//     reference uploads (pinned by tests/golden/camera_goldens.json, which was
+//     generated against the reference's vendored GLM by
+//     oracle/gen_camera_goldens.cpp);
+//   * the uniform block defaults and by-name lookup (shader.hpp:19-69 +
+//     main.cpp:99-120);
+//   * synthetic sweep frames and the row-shard map.
+// Compiled with -ffp-contract=off: every float op is one IEEE binary32 op.
+#include <cmath>
+#include <cstring>
+
+#include "rm_internal.hpp"
+
+namespace {
+
+// ---- GLM 0.9.8.5 restated (column-major mat4: m[col][row]) -------------------
+struct vec3 {
+  float x, y, z;
+};
+struct vec4 {
+  float v[4];
+};
+struct mat4 {
+  vec4 c[4];
+};
+
+// glm::radians  detail/func_trigonometric.inl:12-17
+inline float radians(float deg) { return deg * static_cast<float>(0.01745329251994329576923690768489); }
+// glm::dot (vec3)  detail/func_geometric.inl:54-61  -> (x + y) + z
+inline float dot(vec3 a, vec3 b) {
+  float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+  return tx + ty + tz;
+}
+// glm::normalize  detail/func_geometric.inl:88-96 + inversesqrt func_exponential.inl:130-133
+inline vec3 normalize(vec3 v) {
+  float s = 1.0f / std::sqrt(dot(v, v));
+  return {v.x * s, v.y * s, v.z * s};
+}
+// glm::cross  detail/func_geometric.inl:74-86
+inline vec3 cross(vec3 x, vec3 y) {
+  return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
+}
+inline vec4 add4(vec4 a, vec4 b) {
+  return {{a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]}};
+}
+inline vec4 mul4s(vec4 a, float s) { return {{a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s}}; }
+
+inline mat4 identity() {
+  mat4 m;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) m.c[i].v[j] = (i == j) ? 1.0f : 0.0f;
+  return m;
+}
+
+// glm::rotate(m, angle, v)  gtc/matrix_transform.inl:19-47
+mat4 rotate(const mat4& m, float angle, vec3 v) {
+  const float a = angle;
+  const float c = std::cos(a);
+  const float s = std::sin(a);
+  vec3 axis = normalize(v);
+  vec3 temp = {(1.0f - c) * axis.x, (1.0f - c) * axis.y, (1.0f - c) * axis.z};
+  float R[3][3];
+  R[0][0] = c + temp.x * axis.x;
+  R[0][1] = temp.x * axis.y + s * axis.z;
+  R[0][2] = temp.x * axis.z - s * axis.y;
+  R[1][0] = temp.y * axis.x - s * axis.z;
+  R[1][1] = c + temp.y * axis.y;
+  R[1][2] = temp.y * axis.z + s * axis.x;
+  R[2][0] = temp.z * axis.x + s * axis.y;
+  R[2][1] = temp.z * axis.y - s * axis.x;
+  R[2][2] = c + temp.z * axis.z;
+  mat4 out;
+  for (int i = 0; i < 3; ++i)
+    out.c[i] = add4(add4(mul4s(m.c[0], R[i][0]), mul4s(m.c[1], R[i][1])), mul4s(m.c[2], R[i][2]));
+  out.c[3] = m.c[3];
+  return out;
+}
+
+// mat4 * mat4  detail/type_mat4x4.inl:595-613: ((A0*b0 + A1*b1) + A2*b2) + A3*b3
+mat4 matmul(const mat4& a, const mat4& b) {
+  mat4 r;
+  for (int j = 0; j < 4; ++j)
+    r.c[j] = add4(add4(add4(mul4s(a.c[0], b.c[j].v[0]), mul4s(a.c[1], b.c[j].v[1])),
+                       mul4s(a.c[2], b.c[j].v[2])),
+                  mul4s(a.c[3], b.c[j].v[3]));
+  return r;
+}
+
+// mat4 * vec4  detail/type_mat4x4.inl:501-535: (m0*v0 + m1*v1) + (m2*v2 + m3*v3)
+vec4 matvec(const mat4& m, vec4 v) {
+  vec4 add0 = add4(mul4s(m.c[0], v.v[0]), mul4s(m.c[1], v.v[1]));
+  vec4 add1 = add4(mul4s(m.c[2], v.v[2]), mul4s(m.c[3], v.v[3]));
+  return add4(add0, add1);
+}
+
+inline vec3 ld3(const float* p) { return {p[0], p[1], p[2]}; }
+inline void st3(float* p, vec3 v) {
+  p[0] = v.x;
+  p[1] = v.y;
+  p[2] = v.z;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rm_api_version(void) { return RM_API_VERSION; }
+
+// Camera::Camera(width, height, mouseSensitivity, keyboardSpeed, pos, lookAt, up)
+// camera.cpp:8-14.  As in the reference, the constructor's `up` parameter
+// shadows the member (camera.cpp:13 assigns the parameter), so the member `up`
+// keeps its zero-initialised value (the reference instance is a global,
+// main.cpp:40), as do angleX/angleY/xpos/ypos.  lookAt() overwrites the basis
+// before the first dispatch (main.cpp:97).
+int rm_camera_init(rm_camera_state* c, int32_t width, int32_t height, float mouseSensitivity,
+                   float keyboardSpeed, const float pos[3], const float lookAt[3],
+                   const float up[3]) {
+  if (!c || !pos || !lookAt || !up) return RM_ERR_INVALID;
+  std::memset(c, 0, sizeof(*c));
+  c->width = width;
+  c->height = height;
+  c->mouseSensitivity = mouseSensitivity;
+  c->keyboardSpeed = keyboardSpeed;
+  st3(c->cameraPos, ld3(pos));
+  vec3 p = ld3(pos), l = ld3(lookAt), u = ld3(up);
+  vec3 fwd = normalize({l.x - p.x, l.y - p.y, l.z - p.z});
+  vec3 right = normalize(cross(u, fwd));
+  st3(c->forward, fwd);
+  st3(c->right, right);
+  return RM_OK;
+}
+
+// Camera::setMouse  camera.cpp:16-20
+int rm_camera_set_mouse(rm_camera_state* c, float x, float y) {
+  if (!c) return RM_ERR_INVALID;
+  c->xpos = x;
+  c->ypos = y;
+  return RM_OK;
+}
+
+// Camera::lookAt  camera.cpp:22-51
+int rm_camera_look_at(rm_camera_state* c, int zN, int zP, int xN, int xP, int halfSpeed,
+                      float deltaTime) {
+  if (!c) return RM_ERR_INVALID;
+  c->angleX = c->xpos * c->mouseSensitivity;
+  c->angleY = c->ypos * c->mouseSensitivity;
+  mat4 rotateX = rotate(identity(), radians(c->angleY), {1.0f, 0.0f, 0.0f});
+  mat4 rotateY = rotate(identity(), radians(c->angleX), {0.0f, 1.0f, 0.0f});
+  mat4 R = matmul(rotateY, rotateX);
+  vec4 f4 = matvec(R, {{0.0f, 0.0f, -1.0f, 0.0f}});
+  vec4 u4 = matvec(R, {{0.0f, 1.0f, 0.0f, 0.0f}});
+  vec3 fwd = normalize({f4.v[0], f4.v[1], f4.v[2]});
+  vec3 up = normalize({u4.v[0], u4.v[1], u4.v[2]});
+  vec3 right = normalize(cross(fwd, up));
+  st3(c->forward, fwd);
+  st3(c->up, up);
+  st3(c->right, right);
+  c->keyboardSpeed = halfSpeed ? 5.0f : 10.0f;
+  vec3 pos = ld3(c->cameraPos);
+  auto step = [&](vec3 axis, float sign) {
+    // cameraPos += (keyboardSpeed * (+/-axis)) * deltaTime   camera.cpp:39-50
+    vec3 a = {sign * axis.x, sign * axis.y, sign * axis.z};
+    vec3 k = {c->keyboardSpeed * a.x, c->keyboardSpeed * a.y, c->keyboardSpeed * a.z};
+    pos = {pos.x + k.x * deltaTime, pos.y + k.y * deltaTime, pos.z + k.z * deltaTime};
+  };
+  if (zN) step(fwd, 1.0f);
+  if (zP) step(fwd, -1.0f);
+  if (xN) step(right, -1.0f);
+  if (xP) step(right, 1.0f);
+  st3(c->cameraPos, pos);
+  return RM_OK;
+}
+
+// main.cpp:103-106: setVec4("camera.pos"|"dir"|"yAxis"|"xAxis", v.x, v.y, v.z, 0)
+int rm_camera_to_uniform(const rm_camera_state* c, rm_camera* out) {
+  if (!c || !out) return RM_ERR_INVALID;
+  for (int k = 0; k < 3; ++k) {
+    out->pos[k] = c->cameraPos[k];
+    out->dir[k] = c->forward[k];
+    out->yAxis[k] = c->up[k];
+    out->xAxis[k] = c->right[k];
+  }
+  out->pos[3] = out->dir[3] = out->yAxis[3] = out->xAxis[3] = 0.0f;
+  return RM_OK;
+}
+
+// Defaults: main.cpp:27,30 (AA on, bounce 0), light block main.cpp:108-114,
+// start-up camera main.cpp:40 after lookAt with zero mouse.
+int rm_default_uniforms(rm_uniforms* u) {
+  if (!u) return RM_ERR_INVALID;
+  std::memset(u, 0, sizeof(*u));
+  rm_camera_state cam;
+  const float pos[3] = {0.0f, 0.0f, 0.0f}, look[3] = {0.0f, 0.0f, -1.0f}, up[3] = {0.0f, 1.0f, 0.0f};
+  rm_camera_init(&cam, 1080, 1080, 0.025f, 10.0f, pos, look, up);
+  rm_camera_look_at(&cam, 0, 0, 0, 0, 0, 0.0f);
+  rm_camera_to_uniform(&cam, &u->camera);
+  const float lp[3] = {-5.0f, 5.0f, -10.0f};
+  const float la[3] = {0.03f, 0.04f, 0.1f};
+  const float ld[3] = {0.8f, 0.8f, 0.8f};
+  const float ls[3] = {0.5f, 0.5f, 0.5f};
+  std::memcpy(u->light.position, lp, sizeof lp);
+  std::memcpy(u->light.ambient, la, sizeof la);
+  std::memcpy(u->light.diffuse, ld, sizeof ld);
+  std::memcpy(u->light.specular, ls, sizeof ls);
+  u->light.constant = 1.0f;
+  u->light.linear = 0.009f;
+  u->light.quadratic = 0.00032f;
+  u->iTime = 0.0f;
+  u->bounceVar = 0;
+  u->AA = 1;
+  u->workgroups = 39;  // local_size of computeShader.glsl:12 (ignored)
+  u->mouse[0] = 1.0f;  // MouseInput::EulerAngles() at yaw = pitch = 0 (ignored)
+  u->shadow_mode = RM_SHADOW_SOFT;
+  return RM_OK;
+}
+
+int rm_sweep_uniforms(int32_t frame, int32_t nframes, int32_t bounceVar, int32_t AA,
+                      int32_t shadow_mode, rm_uniforms* out) {
+  if (!out || nframes <= 0 || frame >= nframes || bounceVar < 0 || bounceVar > 5)
+    return RM_ERR_INVALID;
+  rm_default_uniforms(out);
+  rm_camera_state cam;
+  const float look[3] = {0.0f, 0.0f, -1.0f}, up[3] = {0.0f, 1.0f, 0.0f};
+  if (frame < 0) {  // default frame D: the reference's start-up view
+    const float pos[3] = {0.0f, 0.0f, 0.0f};
+    rm_camera_init(&cam, 1080, 1080, 0.025f, 10.0f, pos, look, up);
+    out->iTime = 0.0f;
+  } else {
+    const float pos[3] = {0.0f, 0.0f, 15.0f};
+    rm_camera_init(&cam, 1080, 1080, 0.025f, 10.0f, pos, look, up);
+    double yaw = nframes > 1 ? -20.0 + 40.0 * (double)frame / (double)(nframes - 1) : 0.0;
+    rm_camera_set_mouse(&cam, (float)(yaw / 0.025), (float)(-5.0 / 0.025));
+    out->iTime = (float)frame / 60.0f;
+  }
+  rm_camera_look_at(&cam, 0, 0, 0, 0, 0, 0.0f);
+  rm_camera_to_uniform(&cam, &out->camera);
+  out->bounceVar = bounceVar;
+  out->AA = AA ? 1 : 0;
+  out->shadow_mode = shadow_mode;
+  return RM_OK;
+}
+
+// ---- row sharding: interleaved blocks of row_block rows -------
+int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t* rows_cap) {
+  if (!rows_cap || height <= 0) return RM_ERR_INVALID;
+  if (nshards <= 1) {
+    *rows_cap = height;
+    return RM_OK;
+  }
+  if (row_block <= 0) return RM_ERR_INVALID;
+  int32_t nblocks = (height + row_block - 1) / row_block;
+  int32_t per = (nblocks + nshards - 1) / nshards;
+  *rows_cap = per * row_block;
+  return RM_OK;
+}
+
+int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
+                            int32_t local_row) {
+  if (local_row < 0 || height <= 0) return -1;
+  if (nshards <= 1) return local_row < height ? local_row : -1;
+  if (row_block <= 0 || shard < 0 || shard >= nshards) return -1;
+  int32_t lb = local_row / row_block;
+  int32_t gb = lb * nshards + shard;
+  int32_t g = gb * row_block + local_row % row_block;
+  return g < height ? g : -1;
+}
+
+}  // extern "C"
+
+// ---- uniform lookup by GLSL name (shader.hpp:19-69 semantics) -----------------
+namespace rm {
+
+float* uniform_floats(rm_uniforms* u, const char* name, int* n) {
+  struct Entry {
+    const char* name;
+    size_t off;
+    int n;
+  };
+  static const Entry table[] = {
+      {"camera.pos", offsetof(rm_uniforms, camera.pos), 4},
+      {"camera.dir", offsetof(rm_uniforms, camera.dir), 4},
+      {"camera.yAxis", offsetof(rm_uniforms, camera.yAxis), 4},
+      {"camera.xAxis", offsetof(rm_uniforms, camera.xAxis), 4},
+      {"light.position", offsetof(rm_uniforms, light.position), 3},
+      {"light.ambient", offsetof(rm_uniforms, light.ambient), 3},
+      {"light.diffuse", offsetof(rm_uniforms, light.diffuse), 3},
+      {"light.specular", offsetof(rm_uniforms, light.specular), 3},
+      {"light.constant", offsetof(rm_uniforms, light.constant), 1},
+      {"light.linear", offsetof(rm_uniforms, light.linear), 1},
+      {"light.quadratic", offsetof(rm_uniforms, light.quadratic), 1},
+      {"iTime", offsetof(rm_uniforms, iTime), 1},
+      {"drand48", offsetof(rm_uniforms, drand48), 1},
+      {"mouse", offsetof(rm_uniforms, mouse), 3},
+      {"iMouse", offsetof(rm_uniforms, iMouse), 2},
+  };
+  for (const Entry& e : table)
+    if (std::strcmp(e.name, name) == 0) {
+      *n = e.n;
+      return reinterpret_cast<float*>(reinterpret_cast<char*>(u) + e.off);
+    }
+  return nullptr;
+}
+
+int32_t* uniform_ints(rm_uniforms* u, const char* name) {
+  if (std::strcmp(name, "bounceVar") == 0) return &u->bounceVar;
+  if (std::strcmp(name, "AA") == 0) return &u->AA;
+  if (std::strcmp(name, "shadow_mode") == 0) return &u->shadow_mode;
+  if (std::strcmp(name, "workgroups") == 0) return reinterpret_cast<int32_t*>(&u->workgroups);
+  return nullptr;
+}
+
+}  // namespace rm

@@ -1,0 +1,228 @@
+// rm_kernels.hip — the hot path: per-pixel SDF sphere tracing on gfx950.
+//
+// Reference: shaders/computeShader.glsl:68-344 (dispatched by main.cpp:123).
+// Two kernels compute the same pure function of (pixel, uniforms):
+//   * k_pixel      — one thread per pixel, structured control flow mirroring
+//                    the GLSL call tree (render -> bounce -> softshadow).  The
+//                    straightforward baseline and the debug-counter kernel.
+//   * k_wavequeue  — the performance kernel (rm_wavequeue.hip).
+// See DESIGN.md §4 for the kernel designs and their rooflines.
+#include <hip/hip_runtime.h>
+
+#include "rm_scene.hpp"
+
+namespace rmd {
+
+struct Cnt {
+  uint32_t rays, march, reflect, shadow, normals, lights;
+};
+
+// RayMarch glsl:125-142 / reflectedRay glsl:144-161.  Returns t or -1.
+template <bool COUNT>
+__device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c) {
+  float t = 0.0f;
+  const float tmax = reflected ? 200.0f : 400.0f;
+  const int nmax = reflected ? 256 : 512;
+  for (int i = 0; i < nmax; ++i) {
+    f3 q = add(ro, muls(rd, t));
+    int hid;
+    float d = scene<true>(q, F.blend, F.omblend, hid);
+    if (COUNT) {
+      if (reflected) c.reflect++;
+      else c.march++;
+    }
+    if (d < 0.000001f * t) {
+      id = hid;
+      col = hit_color(hid, q);
+      return t;
+    }
+    if (d > tmax) break;
+    t += d;
+  }
+  id = -1;
+  col = mk(0.0f, 0.0f, 0.0f);
+  return -1.0f;
+}
+
+// GetNormal glsl:278-288
+template <bool COUNT>
+__device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c) {
+  int dummy;
+  if (COUNT) c.normals++;
+  float cc = scene<false>(pos, F.blend, F.omblend, dummy);
+  f3 v = mk(scene<false>(add(pos, mk(0.001f, 0.0f, 0.0f)), F.blend, F.omblend, dummy),
+            scene<false>(add(pos, mk(0.0f, 0.001f, 0.0f)), F.blend, F.omblend, dummy),
+            scene<false>(add(pos, mk(0.0f, 0.0f, 0.001f)), F.blend, F.omblend, dummy));
+  return normalize(subs(v, cc));
+}
+
+// softshadow glsl:201-216
+template <bool COUNT>
+__device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+  float res = 1.0f, t = 0.0f;
+  int dummy;
+  for (int i = 0; i < 16; ++i) {
+    float h = scene<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
+    if (COUNT) c.shadow++;
+    if (h < 0.001f) return 0.05f;
+    res = gmin(res, F.k * h / t);
+    t += h;
+  }
+  return res;
+}
+
+// bounce glsl:163-199 (dead tail skipped; see rm_oracle.h "live" counters)
+template <bool COUNT>
+__device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 primColor,
+                     Cnt& c) {
+  bool prevMatte = false;  // the primary object is never MATTE here (glsl:232-240)
+  f3 prevColor = primColor;
+  f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
+  for (int i = 1; i <= F.bounces; ++i) {
+    // After a MATTE prevObject every remaining iteration is a colour no-op
+    // (glsl:181,189-190): stop instead of running the dead marches.
+    if (prevMatte) break;
+    rayDir = reflect(rayDir, normal);
+    int id;
+    f3 tcol;
+    float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c);
+    pos = add(pos, muls(rayDir, th));
+    // The normal of a miss on the last bounce is never read: skip it.
+    if (th != -1.0f || i < F.bounces) normal = get_normal<COUNT>(F, pos, c);
+    if (th == -1.0f) {
+      tcol = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
+    } else {
+      if (COUNT) c.lights++;
+      tcol = point_light(F, tcol, normal, pos);
+    }
+    if (id == 7 && !prevMatte && i < 3) {
+      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      color = muls(color, sh / (float)i);
+    }
+    color = add(color, divs(mul(tcol, prevColor), (float)i));
+    prevColor = tcol;
+    prevMatte = (id == 7);  // material of the hit: MATTE only for the floor; dummy is 1.0
+  }
+  return color;
+}
+
+// render glsl:218-251
+template <bool COUNT>
+__device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+  f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
+  int id;
+  f3 hcol;
+  float th = march<COUNT>(F, ro, rd, false, id, hcol, c);
+  if (th != -1.0f) {
+    f3 pos = add(ro, muls(rd, th));
+    f3 normal = get_normal<COUNT>(F, pos, c);
+    if (COUNT) c.lights++;
+    color = point_light(F, hcol, normal, pos);
+    if (id == 7) {
+      f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
+      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      color = muls(color, sh);
+      return gamma(color);
+    }
+    if (F.bounces > 0) color = bounce<COUNT>(F, rd, pos, normal, color, hcol, c);
+  }
+  return gamma(color);
+}
+
+// main glsl:291-344, one thread per pixel.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_pixel(Frame F) {
+  const size_t n = (size_t)F.rows * (size_t)F.width;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int lrow = (int)(idx / (size_t)F.width);
+  const int px = (int)(idx - (size_t)lrow * (size_t)F.width);
+  const int py = global_row(F, lrow);
+  Cnt c = {0, 0, 0, 0, 0, 0};
+  float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
+  if (py >= 0) {
+    float x = (float)(px * 2 - F.width) / (float)F.width;
+    float y = (float)(py * 2 - F.height) / (float)F.height;
+    f3 ro, rd;
+    if (F.aa) {
+      const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f};
+      const float oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
+#pragma unroll 1
+      for (int s = 0; s < 4; ++s) {
+        x += ox[s] / (float)F.width;
+        y += oy[s] / (float)F.height;
+        cast_ray(F, x, y, ro, rd);
+        if (COUNT) c.rays++;
+        f3 col = render<COUNT>(F, ro, rd, c);
+        o0 += col.x;
+        o1 += col.y;
+        o2 += col.z;
+      }
+      o0 = o0 / 4.0f;
+      o1 = o1 / 4.0f;
+      o2 = o2 / 4.0f;
+      o3 = 1.0f;
+    } else {
+      cast_ray(F, x, y, ro, rd);
+      if (COUNT) c.rays++;
+      f3 col = render<COUNT>(F, ro, rd, c);
+      o0 = col.x;
+      o1 = col.y;
+      o2 = col.z;
+      o3 = 1.0f;
+    }
+  }
+  store_pixel(F, idx, o0, o1, o2, o3);
+  if (COUNT) {
+    F.sdf_counts[idx] = c.march + c.reflect + c.shadow + 4u * c.normals;
+    atomicAdd(&F.counters[0], (unsigned long long)c.rays);
+    atomicAdd(&F.counters[1], (unsigned long long)c.march);
+    atomicAdd(&F.counters[2], (unsigned long long)c.reflect);
+    atomicAdd(&F.counters[3], (unsigned long long)c.shadow);
+    atomicAdd(&F.counters[4], (unsigned long long)c.normals);
+    atomicAdd(&F.counters[5], (unsigned long long)c.lights);
+  }
+}
+
+// Reassemble [nshards][rows_cap][width] packed shard images into the frame.
+__global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
+                                                 uint32_t* __restrict__ frame, int width,
+                                                 int height, int row_block, int nshards,
+                                                 int rows_cap) {
+  const size_t n = (size_t)width * (size_t)height;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int y = (int)(idx / (size_t)width);
+  const int x = (int)(idx - (size_t)y * (size_t)width);
+  const int b = y / row_block;
+  const int r = b % nshards;
+  const int lrow = (b / nshards) * row_block + y % row_block;
+  frame[idx] = gathered[((size_t)r * rows_cap + lrow) * (size_t)width + x];
+}
+
+}  // namespace rmd
+
+// ---- launch wrappers used by rm_api.hip --------------------------------------
+namespace rm {
+
+hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
+  const size_t n = (size_t)F.rows * (size_t)F.width;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (counters)
+    hipLaunchKernelGGL(rmd::k_pixel<true>, dim3(blocks), dim3(256), 0, s, F);
+  else
+    hipLaunchKernelGGL(rmd::k_pixel<false>, dim3(blocks), dim3(256), 0, s, F);
+  return hipGetLastError();
+}
+
+hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
+                          int nshards, int rows_cap, hipStream_t s) {
+  const size_t n = (size_t)width * (size_t)height;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(rmd::k_unshard, dim3(blocks), dim3(256), 0, s,
+                     static_cast<const uint32_t*>(gathered), static_cast<uint32_t*>(frame), width,
+                     height, row_block, nshards, rows_cap);
+  return hipGetLastError();
+}
+
+}  // namespace rm

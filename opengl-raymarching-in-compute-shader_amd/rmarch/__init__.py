@@ -1,0 +1,422 @@
+"""rmarch — Python host mirror of the reference's host API over librm's C-ABI.
+
+The reference (Qirias/OpenGL-RayMarching-in-Compute-Shader) drives its compute
+shader from C++: a ``Camera`` (source/camera.{hpp,cpp}), a ``Texture``
+(source/texture.{hpp,cpp}), and the program/uniform helpers of
+source/shader.hpp (``CreateCompute``, ``useShader``, ``setFloat`` ...), then
+``glDispatchCompute`` + ``glMemoryBarrier`` (main.cpp:99-125).  This module
+exposes the same names with the same argument meaning on top of librm
+(include/rm_api.h).  The C++ mirror of the same surface is include/rm/*.hpp.
+
+librm has no CPU backend: every render goes through the HIP kernels, and a
+missing ``librm.so`` or a missing GPU raises instead of falling back.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBRM_PATH = os.environ.get("RM_LIBRM", os.path.join(_PKG_DIR, "librm.so"))
+
+# ---- status codes / enums (include/rm_api.h) ---------------------------------
+RM_OK = 0
+RM_WARN_UNKNOWN_UNIFORM = 1
+RM_ERR_INVALID = -1
+RM_ERR_HIP = -2
+RM_ERR_NOMEM = -3
+RM_ERR_NO_DEVICE = -4
+RM_ERR_STATE = -5
+
+RM_OUT_RGBA8 = 1
+RM_OUT_RGBA32F = 2
+RM_SHADOW_SOFT = 0
+RM_SHADOW_HARD = 1
+RM_KERNEL_AUTO = 0
+RM_KERNEL_PIXEL = 1
+RM_KERNEL_WAVEQUEUE = 2
+
+
+class RMError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"librm error {code}: {msg}")
+        self.code = code
+
+
+# ---- POD structs (must match include/rm_api.h exactly) -----------------------
+class rm_camera(C.Structure):
+    _fields_ = [("pos", C.c_float * 4), ("dir", C.c_float * 4),
+                ("yAxis", C.c_float * 4), ("xAxis", C.c_float * 4)]
+
+
+class rm_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("ambient", C.c_float * 3),
+                ("diffuse", C.c_float * 3), ("specular", C.c_float * 3),
+                ("constant", C.c_float), ("linear", C.c_float), ("quadratic", C.c_float)]
+
+
+class rm_uniforms(C.Structure):
+    _fields_ = [("camera", rm_camera), ("light", rm_light), ("iTime", C.c_float),
+                ("bounceVar", C.c_int32), ("AA", C.c_int32), ("workgroups", C.c_uint32),
+                ("drand48", C.c_float), ("mouse", C.c_float * 3), ("iMouse", C.c_float * 2),
+                ("shadow_mode", C.c_int32)]
+
+
+class rm_counters(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("march_steps", C.c_uint64),
+                ("reflect_steps", C.c_uint64), ("shadow_steps", C.c_uint64),
+                ("normals", C.c_uint64), ("lights", C.c_uint64), ("sdf_evals", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+class rm_config(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
+                ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
+                ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32)]
+
+
+class rm_camera_state(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("angleY", C.c_float),
+                ("angleX", C.c_float), ("mouseSensitivity", C.c_float),
+                ("keyboardSpeed", C.c_float), ("xpos", C.c_float), ("ypos", C.c_float),
+                ("cameraPos", C.c_float * 3), ("forward", C.c_float * 3),
+                ("up", C.c_float * 3), ("right", C.c_float * 3)]
+
+
+# ---- library loading --------------------------------------------------------------
+_lib: Optional[C.CDLL] = None
+
+_P = C.c_void_p
+_SIGS = {
+    "rm_api_version": (C.c_int, []),
+    "rm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rm_create": (C.c_int, [C.POINTER(_P), C.POINTER(rm_config)]),
+    "rm_destroy": (None, [_P]),
+    "rm_last_error": (C.c_char_p, [_P]),
+    "rm_set_bool": (C.c_int, [_P, C.c_char_p, C.c_int]),
+    "rm_set_int": (C.c_int, [_P, C.c_char_p, C.c_int32]),
+    "rm_set_uint": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_uint32)]),
+    "rm_set_float": (C.c_int, [_P, C.c_char_p, C.c_float]),
+    "rm_set_vec2": (C.c_int, [_P, C.c_char_p, C.c_float, C.c_float]),
+    "rm_set_vec3": (C.c_int, [_P, C.c_char_p, C.c_float, C.c_float, C.c_float]),
+    "rm_set_vec4": (C.c_int, [_P, C.c_char_p, C.c_float, C.c_float, C.c_float, C.c_float]),
+    "rm_set_uniforms": (C.c_int, [_P, C.POINTER(rm_uniforms)]),
+    "rm_get_uniforms": (C.c_int, [_P, C.POINTER(rm_uniforms)]),
+    "rm_default_uniforms": (C.c_int, [C.POINTER(rm_uniforms)]),
+    "rm_dispatch": (C.c_int, [_P]),
+    "rm_synchronize": (C.c_int, [_P]),
+    "rm_read_rgba8": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
+    "rm_read_rgba32f": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
+    "rm_get_counters": (C.c_int, [_P, C.POINTER(rm_counters)]),
+    "rm_read_sdf_counts": (C.c_int, [_P, _P]),
+    "rm_set_stream": (C.c_int, [_P, _P]),
+    "rm_set_output_rgba8": (C.c_int, [_P, _P]),
+    "rm_get_output_rgba8": (C.c_int, [_P, C.POINTER(_P)]),
+    "rm_unshard_rgba8": (C.c_int, [_P, _P, _P]),
+    "rm_enable_timing": (C.c_int, [_P, C.c_int]),
+    "rm_kernel_time_ms": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]),
+    "rm_shard_rows_cap": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+    "rm_shard_global_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rm_camera_init": (C.c_int, [C.POINTER(rm_camera_state), C.c_int32, C.c_int32, C.c_float,
+                                 C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                 C.POINTER(C.c_float)]),
+    "rm_camera_set_mouse": (C.c_int, [C.POINTER(rm_camera_state), C.c_float, C.c_float]),
+    "rm_camera_look_at": (C.c_int, [C.POINTER(rm_camera_state), C.c_int, C.c_int, C.c_int,
+                                    C.c_int, C.c_int, C.c_float]),
+    "rm_camera_to_uniform": (C.c_int, [C.POINTER(rm_camera_state), C.POINTER(rm_camera)]),
+    "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                    C.POINTER(rm_uniforms)]),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def lib() -> C.CDLL:
+    """Load librm.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIBRM_PATH):
+            raise RuntimeError(
+                f"librm.so not found at {LIBRM_PATH}: build it with `make librm` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIBRM_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, ctx=None) -> int:
+    if rc < 0:
+        msg = lib().rm_last_error(ctx)
+        raise RMError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().rm_device_count(C.byref(n))
+    return n.value
+
+
+# ---- uniforms ------------------------------------------------------------------------
+def default_uniforms() -> rm_uniforms:
+    u = rm_uniforms()
+    _check(lib().rm_default_uniforms(C.byref(u)))
+    return u
+
+
+def sweep_uniforms(frame: int, nframes: int = 120, bounces: int = 0, aa: bool = False,
+                   shadow_mode: int = RM_SHADOW_SOFT) -> rm_uniforms:
+    """Synthetic frame of SURVEY 8(d); frame < 0 = default frame D."""
+    u = rm_uniforms()
+    _check(lib().rm_sweep_uniforms(frame, nframes, bounces, 1 if aa else 0, shadow_mode,
+                                   C.byref(u)))
+    return u
+
+
+# ---- Camera (source/camera.hpp:12-35) --------------------------------------------------
+class Camera:
+    """Mirror of the reference ``Camera`` class (camera.hpp:12-35, camera.cpp:8-51)."""
+
+    def __init__(self, width: int = 1024, height: int = 1024, mouseSensitivity: float = 1.0,
+                 keyboardSpeed: float = 10.0, pos=(0.0, 0.0, 0.0), lookAt=(0.0, 0.0, -1.0),
+                 up=(0.0, 1.0, 0.0)):
+        self._s = rm_camera_state()
+        f3 = C.c_float * 3
+        _check(lib().rm_camera_init(C.byref(self._s), width, height, mouseSensitivity,
+                                    keyboardSpeed, f3(*pos), f3(*lookAt), f3(*up)))
+
+    def setMouse(self, x: float, y: float) -> None:  # camera.cpp:16-20
+        _check(lib().rm_camera_set_mouse(C.byref(self._s), x, y))
+
+    def lookAt(self, zN: bool = False, zP: bool = False, xN: bool = False, xP: bool = False,
+               halfSpeed: bool = False, deltaTime: float = 0.0) -> None:  # camera.cpp:22-51
+        _check(lib().rm_camera_look_at(C.byref(self._s), int(zN), int(zP), int(xN), int(xP),
+                                       int(halfSpeed), deltaTime))
+
+    def to_uniform(self) -> rm_camera:  # main.cpp:103-106
+        c = rm_camera()
+        _check(lib().rm_camera_to_uniform(C.byref(self._s), C.byref(c)))
+        return c
+
+    def __getattr__(self, name):
+        s = object.__getattribute__(self, "_s")
+        v = getattr(s, name)
+        return tuple(v) if isinstance(v, C.Array) else v
+
+    @property
+    def state(self) -> rm_camera_state:
+        return self._s
+
+
+# ---- Texture + compute program (texture.hpp:3-14, shader.hpp) ---------------------------
+class Texture:
+    """Mirror of the reference ``Texture`` (texture.hpp:3-14).
+
+    ``GenerateTexture()`` creates the device image (a librm context);
+    ``texOutput`` is the opaque handle that replaces the GL texture name.
+    """
+
+    def __init__(self, SCREEN_WIDTH: int = 720, SCREEN_HEIGHT: int = 720):
+        self.texWidth = int(SCREEN_WIDTH)
+        self.texHeight = int(SCREEN_HEIGHT)
+        self.texOutput: Optional["Renderer"] = None
+
+    def GenerateTexture(self, outputs: int = RM_OUT_RGBA8 | RM_OUT_RGBA32F,
+                        kernel: int = RM_KERNEL_AUTO, device: int = -1) -> "Renderer":
+        self.texOutput = Renderer(self.texWidth, self.texHeight, outputs=outputs, kernel=kernel,
+                                  device=device)
+        return self.texOutput
+
+
+class Renderer:
+    """One librm context: the compute program bound to its output image."""
+
+    def __init__(self, width: int, height: int, *, outputs: int = RM_OUT_RGBA8,
+                 kernel: int = RM_KERNEL_AUTO, counters: bool = False, device: int = -1,
+                 row_block: int = 0, shard: int = 0, nshards: int = 1):
+        cfg = rm_config(width=width, height=height, device=device, outputs=outputs,
+                        kernel=kernel, counters=1 if counters else 0, row_block=row_block,
+                        shard=shard, nshards=nshards)
+        h = C.c_void_p()
+        _check(lib().rm_create(C.byref(h), C.byref(cfg)))
+        self._h = h
+        self.width, self.height = width, height
+        self.outputs = outputs if outputs else RM_OUT_RGBA8
+        self.nshards, self.shard, self.row_block = max(nshards, 1), shard, row_block
+        self.rows = shard_rows_cap(height, row_block, nshards) if nshards > 1 else height
+
+    # -- lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().rm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -- uniforms by name (shader.hpp:19-69)
+    def setBool(self, name: str, value: bool) -> int:
+        return _check(lib().rm_set_bool(self._h, name.encode(), int(bool(value))), self._h)
+
+    def setInt(self, name: str, value: int) -> int:
+        return _check(lib().rm_set_int(self._h, name.encode(), int(value)), self._h)
+
+    def setuInt(self, name: str, value: int) -> int:
+        v = C.c_uint32(value)
+        return _check(lib().rm_set_uint(self._h, name.encode(), C.byref(v)), self._h)
+
+    def setFloat(self, name: str, value: float) -> int:
+        return _check(lib().rm_set_float(self._h, name.encode(), float(value)), self._h)
+
+    def setVec2(self, name: str, x, y=None) -> int:
+        if y is None:
+            x, y = x
+        return _check(lib().rm_set_vec2(self._h, name.encode(), x, y), self._h)
+
+    def setVec3(self, name: str, x, y=None, z=None) -> int:
+        if y is None:
+            x, y, z = x
+        return _check(lib().rm_set_vec3(self._h, name.encode(), x, y, z), self._h)
+
+    def setVec4(self, name: str, x, y=None, z=None, w=None) -> int:
+        if y is None:
+            x, y, z, w = x
+        return _check(lib().rm_set_vec4(self._h, name.encode(), x, y, z, w), self._h)
+
+    def set_uniforms(self, u: rm_uniforms) -> None:
+        _check(lib().rm_set_uniforms(self._h, C.byref(u)), self._h)
+
+    def get_uniforms(self) -> rm_uniforms:
+        u = rm_uniforms()
+        _check(lib().rm_get_uniforms(self._h, C.byref(u)), self._h)
+        return u
+
+    # -- dispatch / barrier / readback
+    def dispatch(self, u: Optional[rm_uniforms] = None) -> None:
+        """glDispatchCompute (main.cpp:123): asynchronous."""
+        if u is not None:
+            self.set_uniforms(u)
+        _check(lib().rm_dispatch(self._h), self._h)
+
+    def synchronize(self) -> None:
+        """glMemoryBarrier (main.cpp:125) + wait."""
+        _check(lib().rm_synchronize(self._h), self._h)
+
+    def read_rgba8(self, flip_y: bool = False) -> np.ndarray:
+        out = np.empty((self.rows, self.width, 4), np.uint8)
+        _check(lib().rm_read_rgba8(self._h, out.ctypes.data, 0, int(flip_y)), self._h)
+        return out
+
+    def read_rgba32f(self, flip_y: bool = False) -> np.ndarray:
+        out = np.empty((self.rows, self.width, 4), np.float32)
+        _check(lib().rm_read_rgba32f(self._h, out.ctypes.data, 0, int(flip_y)), self._h)
+        return out
+
+    def counters(self) -> dict:
+        c = rm_counters()
+        _check(lib().rm_get_counters(self._h, C.byref(c)), self._h)
+        return c.as_dict()
+
+    def sdf_counts(self) -> np.ndarray:
+        out = np.empty((self.rows, self.width), np.uint32)
+        _check(lib().rm_read_sdf_counts(self._h, out.ctypes.data), self._h)
+        return out
+
+    # -- device interop
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        _check(lib().rm_set_stream(self._h, stream_ptr), self._h)
+
+    def set_output_rgba8(self, device_ptr: Optional[int]) -> None:
+        _check(lib().rm_set_output_rgba8(self._h, device_ptr), self._h)
+
+    def output_rgba8_ptr(self) -> int:
+        p = C.c_void_p()
+        _check(lib().rm_get_output_rgba8(self._h, C.byref(p)), self._h)
+        return p.value or 0
+
+    def unshard_rgba8(self, gathered_ptr: int, frame_ptr: int) -> None:
+        _check(lib().rm_unshard_rgba8(self._h, gathered_ptr, frame_ptr), self._h)
+
+    def enable_timing(self, on: bool = True) -> None:
+        _check(lib().rm_enable_timing(self._h, int(on)), self._h)
+
+    def kernel_time_ms(self, reset: bool = False):
+        ms = C.c_double(0.0)
+        n = C.c_int64(0)
+        _check(lib().rm_kernel_time_ms(self._h, C.byref(ms), C.byref(n), int(reset)), self._h)
+        return ms.value, n.value
+
+
+# shader.hpp-style free functions over a Renderer ("program") ---------------------------
+def CreateCompute(width: int, height: int, **kw) -> Renderer:  # shader.hpp:186-197
+    return Renderer(width, height, **kw)
+
+
+def useShader(program: Renderer) -> None:  # shader.hpp:17 (no global binding state)
+    return None
+
+
+def setBool(p: Renderer, name: str, v) -> int: return p.setBool(name, v)
+def setInt(p: Renderer, name: str, v) -> int: return p.setInt(name, v)
+def setuInt(p: Renderer, name: str, v) -> int: return p.setuInt(name, v)
+def setFloat(p: Renderer, name: str, v) -> int: return p.setFloat(name, v)
+def setVec2(p: Renderer, name: str, *v) -> int: return p.setVec2(name, *v)
+def setVec3(p: Renderer, name: str, *v) -> int: return p.setVec3(name, *v)
+def setVec4(p: Renderer, name: str, *v) -> int: return p.setVec4(name, *v)
+
+
+def glDispatchCompute(p: Renderer) -> None:  # main.cpp:123
+    p.dispatch()
+
+
+def glMemoryBarrier(p: Renderer) -> None:  # main.cpp:125
+    p.synchronize()
+
+
+# ---- row sharding ---------------------------------------------------------
+def shard_rows_cap(height: int, row_block: int, nshards: int) -> int:
+    v = C.c_int32(0)
+    _check(lib().rm_shard_rows_cap(height, row_block, nshards, C.byref(v)))
+    return v.value
+
+
+def shard_global_rows(height: int, row_block: int, shard: int, nshards: int) -> np.ndarray:
+    cap = shard_rows_cap(height, row_block, nshards)
+    return np.array([lib().rm_shard_global_row(height, row_block, shard, nshards, r)
+                     for r in range(cap)], np.int32)
+
+
+def quantize_rgba8(img: np.ndarray) -> np.ndarray:
+    """round(clamp(c,0,1)*255) in float32, NaN -> 0."""
+    c = img.astype(np.float32)
+    v = np.where(c > 0, np.where(c < 1, c, np.float32(1)), np.float32(0)).astype(np.float32)
+    return (v * np.float32(255) + np.float32(0.5)).astype(np.uint8)
+
+
+def write_ppm(path: str, rgba8_top_first: np.ndarray) -> None:
+    """Write an RGBA8 image (top row first) as binary PPM."""
+    h, w = rgba8_top_first.shape[:2]
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h))
+        f.write(np.ascontiguousarray(rgba8_top_first[..., :3]).tobytes())
