@@ -23,7 +23,7 @@ ORACLE   := oracle/_build/librm_oracle.so
 DRIVER   := $(PKG)/rm_frameloop
 
 RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_host.cpp
-RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_internal.hpp include/rm_api.h
+RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp include/rm_api.h
 
 .PHONY: all librm oracle driver goldens clean
 all: librm oracle driver

@@ -54,8 +54,8 @@ extern "C" {
 #define RM_SHADOW_HARD 1 /* extension: k = +inf -> shadow in {0.05, 1}  (BASELINE cfg 1) */
 
 /* ---- kernel variants (rm_config.kernel) ----------------------------------- */
-#define RM_KERNEL_AUTO 0       /* = RM_KERNEL_WAVEQUEUE */
-#define RM_KERNEL_PIXEL 1      /* one thread per pixel, structured control flow */
+#define RM_KERNEL_AUTO 0       /* the fastest measured variant: RM_KERNEL_PIXEL */
+#define RM_KERNEL_PIXEL 1      /* one thread per pixel, 8x8 pixel tile per wave, culled sdf */
 #define RM_KERNEL_WAVEQUEUE 2  /* persistent waves, per-lane job refill (ballot/popc) */
 
 /* Uniform block of computeShader.glsl:7,59-66.  vec4s carry w = 0
@@ -162,6 +162,10 @@ int rm_read_rgba8(rm_ctx *ctx, uint8_t *dst, size_t row_pitch, int flip_y);
 int rm_read_rgba32f(rm_ctx *ctx, float *dst, size_t row_pitch, int flip_y);
 /* Counters of the last dispatch (requires cfg.counters). */
 int rm_get_counters(rm_ctx *ctx, rm_counters *out);
+/* Diagnostic of the wave-queue kernel (requires cfg.counters): loop
+ * iterations summed over all waves of the last dispatch.  SIMD utilisation of
+ * the sdf loop = sdf evaluations / (64 * iterations).  0 for RM_KERNEL_PIXEL. */
+int rm_get_wave_iterations(rm_ctx *ctx, uint64_t *iters);
 /* Per-pixel sdf() evaluation counts of the last dispatch, summed over the
  * pixel's samples, reference units (requires cfg.counters). */
 int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);

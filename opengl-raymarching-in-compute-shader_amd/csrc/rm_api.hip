@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -17,6 +18,8 @@
 #include "rm_scene.hpp"
 
 namespace rm {
+extern int g_wq_batch;
+extern int g_wq_blocks_per_cu;
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
@@ -219,6 +222,9 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   }
   if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
   rm_default_uniforms(&c->u);
+  // Tuning knobs of the wave-queue kernel; defaults are the tuned values.
+  if (const char* e = std::getenv("RM_WQ_BATCH")) rm::g_wq_batch = std::atoi(e);
+  if (const char* e = std::getenv("RM_WQ_BLOCKS_PER_CU")) rm::g_wq_blocks_per_cu = std::atoi(e);
   *out = c;
   return RM_OK;
 }
@@ -317,7 +323,7 @@ int rm_dispatch(rm_ctx* c) {
     e1 = c->ev_pool[c->ev_used].second;
     c->ev_used++;
   }
-  const int kernel = c->cfg.kernel == RM_KERNEL_AUTO ? RM_KERNEL_WAVEQUEUE : c->cfg.kernel;
+  const int kernel = c->cfg.kernel == RM_KERNEL_AUTO ? RM_KERNEL_PIXEL : c->cfg.kernel;
   if (kernel == RM_KERNEL_WAVEQUEUE) {
     RM_HIP(c, hipMemsetAsync(c->d_queue, 0, 256, c->stream));
   }
@@ -397,6 +403,19 @@ int rm_get_counters(rm_ctx* c, rm_counters* out) {
   out->normals = h[4];
   out->lights = h[5];
   out->sdf_evals = h[1] + h[2] + h[3] + 4 * h[4];
+  return RM_OK;
+}
+
+int rm_get_wave_iterations(rm_ctx* c, uint64_t* iters) {
+  if (!c || !iters) return RM_ERR_INVALID;
+  if (!c->cfg.counters) return fail(c, RM_ERR_STATE, "context created without counters");
+  if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  unsigned long long h[8];
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  RM_HIP(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+  *iters = h[6];
   return RM_OK;
 }
 

@@ -23,21 +23,28 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   float t = 0.0f;
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
+  int dummy;
+  bool hit = false;
   for (int i = 0; i < nmax; ++i) {
-    f3 q = add(ro, muls(rd, t));
-    int hid;
-    float d = scene<true>(q, F.blend, F.omblend, hid);
+    const f3 q = add(ro, muls(rd, t));
+    const float d = scene<false>(q, F.blend, F.omblend, dummy);
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
     }
     if (d < 0.000001f * t) {
-      id = hid;
-      col = hit_color(hid, q);
-      return t;
+      hit = true;
+      break;
     }
     if (d > tmax) break;
     t += d;
+  }
+  if (hit) {
+    // the opU id (and colour) of the hit: the same sdf at the same point
+    const f3 q = add(ro, muls(rd, t));
+    scene<true>(q, F.blend, F.omblend, id);
+    col = hit_color(id, q);
+    return t;
   }
   id = -1;
   col = mk(0.0f, 0.0f, 0.0f);
@@ -65,7 +72,7 @@ __device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     float h = scene<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
-    res = gmin(res, F.k * h / t);
+    res = shadow_min(res, F.k, h, t);
     t += h;
   }
   return res;
@@ -129,14 +136,20 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   return gamma(color);
 }
 
-// main glsl:291-344, one thread per pixel.
+// main glsl:291-344, one thread per pixel.  A 256-thread workgroup covers a
+// 16x16 pixel tile and each wave an 8x8 sub-tile, so the 64 rays of a wave
+// are spatially coherent (similar step counts, same culled primitives).
+constexpr int kTile = 16;
+#ifndef RM_PIXEL_MIN_WAVES
+#define RM_PIXEL_MIN_WAVES 6
+#endif
 template <bool COUNT>
-__global__ __launch_bounds__(256) void k_pixel(Frame F) {
-  const size_t n = (size_t)F.rows * (size_t)F.width;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n) return;
-  const int lrow = (int)(idx / (size_t)F.width);
-  const int px = (int)(idx - (size_t)lrow * (size_t)F.width);
+__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int px = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
+  const int lrow = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  if (px >= F.width || lrow >= F.rows) return;
+  const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
   Cnt c = {0, 0, 0, 0, 0, 0};
   float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
@@ -206,12 +219,11 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
 namespace rm {
 
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
-  const size_t n = (size_t)F.rows * (size_t)F.width;
-  const unsigned blocks = (unsigned)((n + 255) / 256);
+  const dim3 grid((F.width + rmd::kTile - 1) / rmd::kTile, (F.rows + rmd::kTile - 1) / rmd::kTile);
   if (counters)
-    hipLaunchKernelGGL(rmd::k_pixel<true>, dim3(blocks), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(256), 0, s, F);
   else
-    hipLaunchKernelGGL(rmd::k_pixel<false>, dim3(blocks), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(256), 0, s, F);
   return hipGetLastError();
 }
 

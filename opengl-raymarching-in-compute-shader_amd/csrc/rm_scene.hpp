@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rm_fastmath.hpp"
+
 namespace rmd {
 
 struct f3 {
@@ -32,6 +34,19 @@ __device__ __forceinline__ f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, 
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / __builtin_sqrtf(dot(a, a))); }
+// v_min_f32 / v_min3_f32 without the NaN-quieting canonicalisations LLVM adds
+// when it cannot prove an operand canonical (values merged from branches).
+// All operands here are finite sdf values or +inf, never NaN.
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 // GLSL min/max (y < x ? y : x) — used where a signed zero or NaN could differ.
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
@@ -59,53 +74,215 @@ struct Frame {
 };
 
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
-// Capsule constants (glsl:120): ba = b - a and dot(ba, ba), folded in float.
-constexpr float CAP_AX = -0.1f, CAP_AY = 0.1f, CAP_AZ = -0.1f;
-constexpr float CAP_BAX = 2.0f - CAP_AX, CAP_BAY = 4.0f - CAP_AY, CAP_BAZ = 2.0f - CAP_AZ;
-constexpr float CAP_BB = (CAP_BAX * CAP_BAX + CAP_BAY * CAP_BAY) + CAP_BAZ * CAP_BAZ;
-
 // Minimum scene distance and the opU id (glsl:107-123).  `id` follows opU's
 // rule exactly: a later primitive replaces the running one unless the running
 // distance is strictly smaller.  blend/omblend carry mix()'s a and 1-a.
-template <bool WANT_ID>
-__device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id) {
+//
+// SAFE = false uses the cheap exact sequences of rm_fastmath.hpp (sqrt_core,
+// div_capbb), each exact on its proven domain; any lane whose operands leave
+// that domain (a sqrt argument in (0, 2^-96), |capsule numerator| < 2^-100)
+// sets `tiny`, and scene() recomputes those lanes with SAFE = true (the full
+// correctly-rounded forms).  Either way the result is the IEEE value.
+template <bool WANT_ID, bool SAFE>
+__device__ __forceinline__ float scene_impl(f3 p, float blend, float omblend, int& id, bool& tiny) {
+  auto SQ = [](float x) { return SAFE ? sqrt_cr_nonneg(x) : sqrt_core(x); };
   // sphere (15,0,-10) r3, id 0   glsl:111
-  float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
-  float d = __builtin_sqrtf((ax * ax + ay * ay) + az * az) - 3.0f;
+  const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
+  const float ay2 = ay * ay, az2 = az * az;
+  const float x0 = (ax * ax + ay2) + az2;
+  float d = SQ(x0) - 3.0f;
   if (WANT_ID) id = 0;
   // sphere (-25,0,-10) r3, id 1  glsl:112
-  float bx = p.x + 25.0f;
-  float d1 = __builtin_sqrtf((bx * bx + ay * ay) + az * az) - 3.0f;
+  const float bx = p.x + 25.0f;
+  const float x1 = (bx * bx + ay2) + az2;
+  const float d1 = SQ(x1) - 3.0f;
   if (WANT_ID) id = (d < d1) ? id : 1;
   d = fminf(d, d1);
-  // mix(box, sphere, blend) at (-5,0,-10), id 4   glsl:115-117
-  float cx = p.x + 5.0f;
-  float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
-  float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
-  float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + __builtin_sqrtf((mx * mx + my * my) + mz * mz);
-  float sph = __builtin_sqrtf((cx * cx + ay * ay) + az * az) - 3.0f;
-  float d4 = box * omblend + sph * blend;
+  // mix(box, sphere, blend) at (-5,0,-10), id 4   glsl:87-91,115-117
+  const float cx = p.x + 5.0f;
+  const float cx2 = cx * cx;
+  const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
+  const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
+  const float xb = (mx * mx + my * my) + mz * mz;
+  const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + SQ(xb);
+  const float xs = (cx2 + ay2) + az2;
+  const float sph = SQ(xs) - 3.0f;
+  const float d4 = box * omblend + sph * blend;
   if (WANT_ID) id = (d < d4) ? id : 4;
   d = fminf(d, d4);
   // torus at (-5,0,10), (pos - c).xzy, t = (2.5, 0.5), id 5   glsl:93-96,119
-  float tz = p.z - 10.0f;
-  float l = __builtin_sqrtf(cx * cx + ay * ay) - 2.5f;
-  float d5 = __builtin_sqrtf(l * l + tz * tz) - 0.5f;
+  const float tz = p.z - 10.0f;
+  const float xt1 = cx2 + ay2;
+  const float l = SQ(xt1) - 2.5f;
+  const float xt2 = l * l + tz * tz;
+  const float d5 = SQ(xt2) - 0.5f;
   if (WANT_ID) id = (d < d5) ? id : 5;
   d = fminf(d, d5);
   // capsule at (-5,-2,-30), a(-.1,.1,-.1) b(2,4,2) r1, id 6   glsl:98-103,120
-  float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
-  float h = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
-  h = fminf(fmaxf(h / CAP_BB, 0.0f), 1.0f);
-  float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
-  float d6 = __builtin_sqrtf((ex * ex + ey * ey) + ez * ez) - 1.0f;
+  const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
+  const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
+  float h = SAFE ? hn / CAP_BB_HOST : div_capbb(hn);
+  h = fminf(fmaxf(h, 0.0f), 1.0f);
+  const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
+  const float xc = (ex * ex + ey * ey) + ez * ez;
+  const float d6 = SQ(xc) - 1.0f;
   if (WANT_ID) id = (d < d6) ? id : 6;
   d = fminf(d, d6);
   // plane y = -5.5, id 7 (MATTE)   glsl:85,121
-  float d7 = p.y + 5.5f;
+  const float d7 = p.y + 5.5f;
   if (WANT_ID) id = (d < d7) ? id : 7;
   d = fminf(d, d7);
+  if (!SAFE) {
+    // operands outside the fast sequences' proven domains (see above)
+    const float m = fminf(fminf(fminf(x0, x1), fminf(xs, xt1)), fminf(xt2, xc));
+    tiny = (m < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN)) |
+           (fabsf(hn) < DIV_CAPBB_MIN);
+  }
   return d;
+}
+
+// ---- scene with exact bounding-sphere culling --------------------------------
+// Same value and id as scene_impl.  Each expensive primitive k gets a lower
+// bound LB_k <= its float sdf and the plane/spheres/blend give an upper bound
+// U >= the float minimum, from raw v_sqrt_f32 (within 1.5 ulp, see
+// rm_fastmath.hpp) widened by a relative 2^-12 and an absolute 2^-18 margin.
+// If LB_k > U the primitive is strictly farther than the minimum: it can
+// neither be the minimum nor tie it (opU ties go to the later primitive), so
+// skipping it changes nothing.  A primitive is evaluated exactly when any lane
+// of the wave needs it (the branch is skipped only when no lane does).
+//   bounding spheres (centre, radius):   sdf >= |p - c| - R   and, for U,
+//   sphere  (15,0,-10) / (-25,0,-10): R = 3 (exact: sdf = |p - c| - 3)
+//   box/sphere blend (-5,0,-10): R = |(3,2.5,2.5)| = 4.6368 (box circumradius);
+//                                upper bound |p - c| - 2.5 (box inradius)
+//   torus (-5,0,10): R = 2.5 + 0.5
+//   capsule: centre = midpoint of a..b = (-4.05,0.05,-29.05), R = |b-a|/2 + 1
+constexpr float CULL_REL_LO = 1.0f - 0x1p-12f;
+constexpr float CULL_REL_HI = 1.0f + 0x1p-12f;
+constexpr float CULL_ABS = 0x1p-18f;
+constexpr float R_BLEND_LO = 4.63682f;   // >= sqrt(3^2 + 2.5^2 + 2.5^2) = 4.636809
+constexpr float R_TORUS = 3.0f;
+constexpr float R_CAPSULE = 3.45115f;    // >= sqrt(24.03)/2 + 1 = 3.451050
+constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;
+
+#ifdef RM_STATS
+// Diagnostic build only: wave-level counts of exact primitive evaluations.
+__device__ unsigned long long g_stats[16];
+#define RM_STAT(k)                                                   \
+  do {                                                               \
+    if (__lane_id() == __builtin_ffsll(__ballot(1)) - 1) atomicAdd(&g_stats[k], 1ull); \
+  } while (0)
+#else
+#define RM_STAT(k) \
+  do {             \
+  } while (0)
+#endif
+
+template <bool WANT_ID>
+__device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, int& id, bool& tiny) {
+  // centre offsets and squared centre distances (shared sub-terms)
+  const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
+  const float bx = p.x + 25.0f, cx = p.x + 5.0f, tz = p.z - 10.0f;
+  const float ay2 = ay * ay, az2 = az * az, cx2 = cx * cx;
+  const float x0 = (ax * ax + ay2) + az2;     // sphere 0 (exact sdf argument)
+  const float x1 = (bx * bx + ay2) + az2;     // sphere 1 (exact sdf argument)
+  const float xs = (cx2 + ay2) + az2;         // blend centre (= its sphere's argument)
+  const float xt1 = cx2 + ay2;                // torus inner argument
+  const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
+  const float xtc = xt1 + tz * tz;            // torus centre (bound only)
+  const float xk = (kx * kx + ky * ky) + kz * kz;  // capsule centre (bound only)
+  const float r0 = __builtin_amdgcn_sqrtf(x0), r1 = __builtin_amdgcn_sqrtf(x1);
+  const float rs = __builtin_amdgcn_sqrtf(xs), rt = __builtin_amdgcn_sqrtf(xtc);
+  const float rk = __builtin_amdgcn_sqrtf(xk);
+  const float d7 = p.y + 5.5f;  // plane, exact (glsl:85,121)
+  // upper bound of the minimum
+  float U = fminf(d7, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
+  U = fminf(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f));
+  U = fminf(U, __builtin_fmaf(rs, CULL_REL_HI, CULL_ABS - 2.5f));
+  RM_STAT(0);
+  const float INF = __builtin_huge_valf();
+  float d0 = INF, d1 = INF, d4 = INF, d5 = INF, d6 = INF;
+  bool tn = false;
+  if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    RM_STAT(1);
+    d0 = sqrt_core(x0) - 3.0f;  // glsl:111
+    tn |= x0 < SQRT_CORE_MIN;
+  }
+  if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    RM_STAT(2);
+    d1 = sqrt_core(x1) - 3.0f;  // glsl:112
+    tn |= x1 < SQRT_CORE_MIN;
+  }
+  if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {  // glsl:87-91,115-117
+    RM_STAT(3);
+    const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
+    const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
+    const float xb = (mx * mx + my * my) + mz * mz;
+    const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + sqrt_core(xb);
+    const float sph = sqrt_core(xs) - 3.0f;
+    d4 = box * omblend + sph * blend;
+    tn |= (xs < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN));
+  }
+  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {  // glsl:93-96,119
+    RM_STAT(4);
+    const float l = sqrt_core(xt1) - 2.5f;
+    const float xt2 = l * l + tz * tz;
+    d5 = sqrt_core(xt2) - 0.5f;
+    tn |= (xt1 < SQRT_CORE_MIN) | (xt2 < SQRT_CORE_MIN);
+  }
+  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {  // glsl:98-103,120
+    RM_STAT(5);
+    const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
+    const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
+    const float h = fminf(fmaxf(div_capbb(hn), 0.0f), 1.0f);
+    const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
+    const float xc = (ex * ex + ey * ey) + ez * ez;
+    d6 = sqrt_core(xc) - 1.0f;
+    tn |= (xc < SQRT_CORE_MIN) | (fabsf(hn) < DIV_CAPBB_MIN);
+  }
+  tiny = tn;
+  // opU chain in the reference order (glsl:111-121); culled entries are +inf
+  float d = d0;
+  if (WANT_ID) {
+    id = 0;
+    id = (d < d1) ? id : 1;
+    d = vmin(d, d1);
+    id = (d < d4) ? id : 4;
+    d = vmin(d, d4);
+    id = (d < d5) ? id : 5;
+    d = vmin(d, d5);
+    id = (d < d6) ? id : 6;
+    d = vmin(d, d6);
+    id = (d < d7) ? id : 7;
+    d = vmin(d, d7);
+  } else {
+    d = vmin3(vmin3(d, d1, d4), vmin(d5, d6), d7);
+  }
+  return d;
+}
+
+#ifndef RM_SCENE_CULL
+#define RM_SCENE_CULL 1
+#endif
+
+template <bool WANT_ID>
+__device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id) {
+  bool tiny = false;
+  float d = RM_SCENE_CULL ? scene_cull<WANT_ID>(p, blend, omblend, id, tiny)
+                          : scene_impl<WANT_ID, false>(p, blend, omblend, id, tiny);
+  if (__builtin_expect(tiny, 0)) d = scene_impl<WANT_ID, true>(p, blend, omblend, id, tiny);
+  return d;
+}
+
+// softshadow's  res = min(res, k * h / t)  (glsl:211), exactly.  The quotient
+// only matters when it is below res, so it is first bounded with v_rcp_f32
+// (within 1 ulp): if (k*h)*rcp(t) exceeds res by a 2^-16 relative margin the
+// exact quotient does too and res is unchanged; otherwise the correctly
+// rounded division decides.  k = +inf (hard shadows) gives +inf: unchanged.
+__device__ __forceinline__ float shadow_min(float res, float k, float h, float t) {
+  const float kh = k * h;
+  const float qa = kh * __builtin_amdgcn_rcpf(t);
+  if (qa > res * (1.0f + 0x1p-16f)) return res;
+  return gmin(res, kh / t);
 }
 
 // checkers(p) glsl:77-80

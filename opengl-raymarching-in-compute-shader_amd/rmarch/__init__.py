@@ -114,6 +114,7 @@ _SIGS = {
     "rm_read_rgba32f": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
     "rm_get_counters": (C.c_int, [_P, C.POINTER(rm_counters)]),
     "rm_read_sdf_counts": (C.c_int, [_P, _P]),
+    "rm_get_wave_iterations": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "rm_set_stream": (C.c_int, [_P, _P]),
     "rm_set_output_rgba8": (C.c_int, [_P, _P]),
     "rm_get_output_rgba8": (C.c_int, [_P, C.POINTER(_P)]),
@@ -337,6 +338,11 @@ class Renderer:
         c = rm_counters()
         _check(lib().rm_get_counters(self._h, C.byref(c)), self._h)
         return c.as_dict()
+
+    def wave_iterations(self) -> int:
+        v = C.c_uint64(0)
+        _check(lib().rm_get_wave_iterations(self._h, C.byref(v)), self._h)
+        return int(v.value)
 
     def sdf_counts(self) -> np.ndarray:
         out = np.empty((self.rows, self.width), np.uint32)

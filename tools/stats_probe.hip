@@ -1,0 +1,21 @@
+// Diagnostic: per-primitive wave-level exact-evaluation rates of scene_cull in k_pixel.
+#define RM_STATS 1
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_kernels.hip"
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_api.hip"
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_wavequeue.hip"
+#include <cstdio>
+int main(int argc, char** argv) {
+  int kernel = argc > 1 ? atoi(argv[1]) : RM_KERNEL_PIXEL;
+  rm_config cfg = {3840, 2160, 0, RM_OUT_RGBA8, kernel, 0, 0, 0, 1};
+  rm_ctx* c; if (rm_create(&c, &cfg)) { printf("create failed %s\n", rm_last_error(nullptr)); return 1; }
+  rm_uniforms u; rm_sweep_uniforms(30, 120, 3, 1, 0, &u); rm_set_uniforms(c, &u);
+  unsigned long long z[16] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_stats), z, sizeof z);
+  rm_dispatch(c); rm_synchronize(c);
+  unsigned long long h[16];
+  hipMemcpyFromSymbol(h, HIP_SYMBOL(rmd::g_stats), sizeof h);
+  const char* nm[] = {"wave-sdf", "sphere0", "sphere1", "blend", "torus", "capsule"};
+  for (int k = 0; k < 6; ++k) printf("%-10s %12llu  %.3f\n", nm[k], h[k], (double)h[k] / h[0]);
+  rm_destroy(c);
+  return 0;
+}
