@@ -144,6 +144,14 @@ def lib() -> C.CDLL:
             raise RuntimeError(
                 f"librm.so not found at {LIBRM_PATH}: build it with `make librm` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
+        # PyTorch-ROCm bundles its own libamdhip64.so.7.  Load it first so that
+        # librm binds to the same HIP runtime (same SONAME) and device
+        # pointers / streams / RCCL buffers are shared with torch; loading
+        # librm first would bring /opt/rocm's copy in as a second runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIBRM_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
