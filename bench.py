@@ -82,7 +82,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="wavequeue", choices=["wavequeue", "pixel"])
+    ap.add_argument("--kernel", default="pixel", choices=["pixel", "wavequeue"],
+                    help="pixel = k_pixel (RM_KERNEL_AUTO's choice), wavequeue = k_wavequeue")
     ap.add_argument("--row-block", type=int, default=8,
                     help="rows per interleaved block when sharding over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")

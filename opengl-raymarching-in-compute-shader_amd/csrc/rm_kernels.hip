@@ -11,6 +11,10 @@
 
 #include "rm_scene.hpp"
 
+#ifndef RM_LAZY_CULL
+#define RM_LAZY_CULL 1
+#endif
+
 namespace rmd {
 
 struct Cnt {
@@ -25,9 +29,19 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   const int nmax = reflected ? 256 : 512;
   int dummy;
   bool hit = false;
+#if RM_LAZY_CULL
+  LazyCull lc;
+  lazy_init(lc, ro, rd);
+#endif
   for (int i = 0; i < nmax; ++i) {
     const f3 q = add(ro, muls(rd, t));
+#if RM_LAZY_CULL
+    bool tiny = false;
+    float d = scene_lazy<false>(q, t, lc, F.blend, F.omblend, dummy, tiny);
+    if (__builtin_expect(tiny, 0)) d = scene_impl<false, true>(q, F.blend, F.omblend, dummy, tiny);
+#else
     const float d = scene<false>(q, F.blend, F.omblend, dummy);
+#endif
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
@@ -197,6 +211,64 @@ __global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
   }
 }
 
+// main glsl:291-344 with 4x supersampling, one thread per (pixel, sample).
+// The 4 samples of a pixel sit in 4 adjacent lanes, so a wave covers a 4x4
+// pixel tile with all its samples (the most coherent 64 rays available: the
+// sample rays of one pixel are sub-pixel apart).  Lane s re-forms the
+// cumulative uv of glsl:311-332 with the same sequential float adds, and lane
+// s == 0 sums the samples in the reference's fixed order ((c0+c1)+c2)+c3 via
+// lane shuffles before the /4 (glsl:315-335).
+constexpr int kSampleTile = 8;  // 8x8 pixels per 256-thread workgroup
+template <bool COUNT>
+__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_sample(Frame F) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s = lane & 3, q = lane >> 2;
+  const int px = blockIdx.x * kSampleTile + (wave & 1) * 4 + (q & 3);
+  const int lrow = blockIdx.y * kSampleTile + (wave >> 1) * 4 + (q >> 2);
+  if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
+  const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
+  const int py = global_row(F, lrow);
+  Cnt c = {0, 0, 0, 0, 0, 0};
+  f3 col = mk(0.0f, 0.0f, 0.0f);
+  if (py >= 0) {
+    float x = (float)(px * 2 - F.width) / (float)F.width;
+    float y = (float)(py * 2 - F.height) / (float)F.height;
+    const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f};
+    const float oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
+    for (int j = 0; j <= s; ++j) {
+      x += ox[j] / (float)F.width;
+      y += oy[j] / (float)F.height;
+    }
+    f3 ro, rd;
+    cast_ray(F, x, y, ro, rd);
+    if (COUNT) c.rays++;
+    col = render<COUNT>(F, ro, rd, c);
+  }
+  const float r1 = __shfl(col.x, lane + 1), g1 = __shfl(col.y, lane + 1), b1 = __shfl(col.z, lane + 1);
+  const float r2 = __shfl(col.x, lane + 2), g2 = __shfl(col.y, lane + 2), b2 = __shfl(col.z, lane + 2);
+  const float r3 = __shfl(col.x, lane + 3), g3 = __shfl(col.y, lane + 3), b3 = __shfl(col.z, lane + 3);
+  uint32_t cnt = 0;
+  if (COUNT) {
+    const uint32_t mine = c.march + c.reflect + c.shadow + 4u * c.normals;
+    cnt = mine + __shfl(mine, lane + 1) + __shfl(mine, lane + 2) + __shfl(mine, lane + 3);
+    atomicAdd(&F.counters[0], (unsigned long long)c.rays);
+    atomicAdd(&F.counters[1], (unsigned long long)c.march);
+    atomicAdd(&F.counters[2], (unsigned long long)c.reflect);
+    atomicAdd(&F.counters[3], (unsigned long long)c.shadow);
+    atomicAdd(&F.counters[4], (unsigned long long)c.normals);
+    atomicAdd(&F.counters[5], (unsigned long long)c.lights);
+  }
+  if (s != 0) return;
+  if (py >= 0) {
+    const float o0 = ((col.x + r1) + r2) + r3, o1 = ((col.y + g1) + g2) + g3,
+                o2 = ((col.z + b1) + b2) + b3;
+    store_pixel(F, idx, o0 / 4.0f, o1 / 4.0f, o2 / 4.0f, 1.0f);
+  } else {
+    store_pixel(F, idx, 0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  if (COUNT) F.sdf_counts[idx] = cnt;
+}
+
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
@@ -219,6 +291,15 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
 namespace rm {
 
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
+  if (F.aa) {
+    const dim3 g((F.width + rmd::kSampleTile - 1) / rmd::kSampleTile,
+                 (F.rows + rmd::kSampleTile - 1) / rmd::kSampleTile);
+    if (counters)
+      hipLaunchKernelGGL(rmd::k_sample<true>, g, dim3(256), 0, s, F);
+    else
+      hipLaunchKernelGGL(rmd::k_sample<false>, g, dim3(256), 0, s, F);
+    return hipGetLastError();
+  }
   const dim3 grid((F.width + rmd::kTile - 1) / rmd::kTile, (F.rows + rmd::kTile - 1) / rmd::kTile);
   if (counters)
     hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(256), 0, s, F);

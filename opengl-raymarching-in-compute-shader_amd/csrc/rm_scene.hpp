@@ -260,6 +260,137 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   return d;
 }
 
+// ---- scene with LAZY culling along a ray ----------------------------------------
+// For a march p(t) = ro + rd*t.  Primitive k is skipped while t < te[k].  When a
+// primitive is re-tested at p_i (t_i) with upper bound U_i >= min(p_i) and
+// lower bound LB_k(p_i) <= sdf_k(p_i), and LB_k > U_i, then for any later
+// point p_j on the ray, by the 1-Lipschitz property of the distances,
+//   sdf_k(p_j) - min(p_j) >= (LB_k - U_i) - 2 |p_j - p_i|,  |p_j - p_i| ~ |rd| (t_j - t_i),
+// so k stays strictly above the minimum (cannot be it, cannot tie it) while
+//   t_j < te_k = t_i + (LB_k - U_i - slack) / (2 |rd| (1 + 2^-10)).
+// `slack` covers the float error of the evaluated sdfs and of p(t) itself
+// (relative 2^-14 of |ro|_1 + |rd| t + 64 — generous against ~2^-21 actual).
+// A primitive whose bound does not cull it is evaluated exactly and re-tested
+// at the next step.  U_i = min(plane, exact values evaluated so far this
+// step).  The minimum and the opU id are merged in the reference order, so the
+// result equals scene_impl's.
+struct LazyCull {
+  float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
+  float temin;   // min over te[]
+  float rdlen;   // |rd| (upper-rounded)
+  float ro1;     // |ro|_1
+};
+
+__device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
+  const float NEG = -__builtin_huge_valf();
+#pragma unroll
+  for (int k = 0; k < 5; ++k) c.te[k] = NEG;
+  c.temin = NEG;
+  c.rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);
+  c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
+}
+
+template <bool WANT_ID>
+__device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend, float omblend,
+                                            int& id, bool& tiny) {
+  const float INF = __builtin_huge_valf();
+  const float d7 = p.y + 5.5f;  // plane, exact (glsl:85,121)
+  float d0 = INF, d1 = INF, d4 = INF, d5 = INF, d6 = INF;
+  bool tn = false;
+  if (t >= lc.temin) {
+    float U = d7;
+    const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
+    const float inv2v = 0.5f * (1.0f - 0x1p-10f) / lc.rdlen;
+    // expiry update: k stays culled while the ray travels (lb - U - slack)/2
+    auto retest = [&](float x, float R, float& te) -> bool {  // true: evaluate exactly
+      const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
+      const float m = lb - U - slack;
+      if (m > 0.0f) {
+        te = __builtin_fmaf(m, inv2v, t);
+        return false;
+      }
+      te = t;
+      return true;
+    };
+    const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
+    const float ay2 = ay * ay, az2 = az * az;
+    const float cx = p.x + 5.0f, cx2 = cx * cx;
+    if (t >= lc.te[0]) {  // sphere (15,0,-10) r3, glsl:111
+      const float x0 = (ax * ax + ay2) + az2;
+      if (retest(x0, 3.0f, lc.te[0])) {
+        d0 = sqrt_core(x0) - 3.0f;
+        U = vmin(U, d0);
+        tn |= x0 < SQRT_CORE_MIN;
+      }
+    }
+    if (t >= lc.te[1]) {  // sphere (-25,0,-10) r3, glsl:112
+      const float bx = p.x + 25.0f;
+      const float x1 = (bx * bx + ay2) + az2;
+      if (retest(x1, 3.0f, lc.te[1])) {
+        d1 = sqrt_core(x1) - 3.0f;
+        U = vmin(U, d1);
+        tn |= x1 < SQRT_CORE_MIN;
+      }
+    }
+    if (t >= lc.te[2]) {  // box/sphere blend, glsl:87-91,115-117
+      const float xs = (cx2 + ay2) + az2;
+      if (retest(xs, R_BLEND_LO, lc.te[2])) {
+        const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
+        const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
+        const float xb = (mx * mx + my * my) + mz * mz;
+        const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + sqrt_core(xb);
+        const float sph = sqrt_core(xs) - 3.0f;
+        d4 = box * omblend + sph * blend;
+        U = vmin(U, d4);
+        tn |= (xs < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN));
+      }
+    }
+    if (t >= lc.te[3]) {  // torus, glsl:93-96,119
+      const float tz = p.z - 10.0f;
+      const float xt1 = cx2 + ay2;
+      if (retest(xt1 + tz * tz, R_TORUS, lc.te[3])) {
+        const float l = sqrt_core(xt1) - 2.5f;
+        const float xt2 = l * l + tz * tz;
+        d5 = sqrt_core(xt2) - 0.5f;
+        U = vmin(U, d5);
+        tn |= (xt1 < SQRT_CORE_MIN) | (xt2 < SQRT_CORE_MIN);
+      }
+    }
+    if (t >= lc.te[4]) {  // capsule, glsl:98-103,120
+      const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
+      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
+        const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
+        const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
+        const float h = fminf(fmaxf(div_capbb(hn), 0.0f), 1.0f);
+        const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
+        const float xc = (ex * ex + ey * ey) + ez * ez;
+        d6 = sqrt_core(xc) - 1.0f;
+        U = vmin(U, d6);
+        tn |= (xc < SQRT_CORE_MIN) | (fabsf(hn) < DIV_CAPBB_MIN);
+      }
+    }
+    lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
+  }
+  tiny = tn;
+  float d = d0;
+  if (WANT_ID) {
+    id = 0;
+    id = (d < d1) ? id : 1;
+    d = vmin(d, d1);
+    id = (d < d4) ? id : 4;
+    d = vmin(d, d4);
+    id = (d < d5) ? id : 5;
+    d = vmin(d, d5);
+    id = (d < d6) ? id : 6;
+    d = vmin(d, d6);
+    id = (d < d7) ? id : 7;
+    d = vmin(d, d7);
+  } else {
+    d = vmin3(vmin3(d, d1, d4), vmin(d5, d6), d7);
+  }
+  return d;
+}
+
 #ifndef RM_SCENE_CULL
 #define RM_SCENE_CULL 1
 #endif
