@@ -15,7 +15,7 @@ shadows, 4x supersampling, 1 MI355X.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  Extra objects:
-  roofline     : FP32-VALU roofline of the dominant kernel (k_wavequeue);
+  roofline     : FP32-VALU roofline of the dominant kernel (k_sample / k_pixel);
                  achieved = algorithmic ops per launch (SURVEY 8(d) weights x the
                  exact work counters of the frames rendered) / mean kernel time
                  measured with HIP events on the launch stream.
@@ -67,6 +67,23 @@ def algorithmic_ops(c: dict) -> int:
     return (OPS["march"] * c["march_steps"] + OPS["reflect"] * c["reflect_steps"]
             + OPS["shadow"] * c["shadow_steps"] + OPS["normal"] * c["normals"]
             + OPS["light"] * c["lights"] + OPS["ray"] * c["rays"])
+
+
+def pmc_traffic(kernel_name: str, workload: str):
+    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary
+    (profiles/rNN_pmc.json, FETCH_SIZE/WRITE_SIZE passes of tools/profile_round.sh)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("_meta", {}).get("workload") != workload:
+            continue
+        for k, v in d.items():
+            if kernel_name in k and "hbm_bytes_per_launch" in v:
+                return int(v["hbm_bytes_per_launch"]), os.path.basename(path)
+    return None, None
 
 
 def dist_env():
@@ -184,6 +201,8 @@ def main() -> int:
             ops_total += algorithmic_ops(c)
             cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
     mean_kernel_ms = kernel_ms / max(launches, 1)
+    kname = ("k_sample" if cfg["aa"] else "k_pixel") if args.kernel == "pixel" else "k_wavequeue"
+    traffic, traffic_src = pmc_traffic(kname + "<false>", f"cfg{args.config}")
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
     bytes_per_launch = r.rows * W * 4
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
@@ -229,15 +248,15 @@ def main() -> int:
             "config": {"workload": f"cfg{args.config}: {cfg['desc']}", "width": W, "height": H,
                        "bounces": cfg["bounces"], "aa": cfg["aa"],
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
-                       "kernel": f"k_{args.kernel}",
+                       "kernel": kname,
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        if ws > 1 else "single GPU")},
             "fps": round(frames / elapsed, 3),
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3),
                          "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
-                         "traffic": None,
-                         "kernel": f"k_{args.kernel}", "mean_kernel_ms": round(mean_kernel_ms, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
                          "ops_per_launch": int(ops_total / max(launches, 1)),
                          "hbm_write_GBs": round(hbm_gbs, 2),
                          "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
