@@ -34,11 +34,18 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   lazy_init(lc, ro, rd);
 #endif
   for (int i = 0; i < nmax; ++i) {
+#ifdef RM_STATS
+    {
+      const unsigned long long m = __ballot(1);
+      if (__lane_id() == __builtin_ffsll(m) - 1) {
+        atomicAdd(&g_stats[reflected ? 6 : 15], 1ull);
+        atomicAdd(&g_stats[7], (unsigned long long)__popcll(m));
+      }
+    }
+#endif
     const f3 q = add(ro, muls(rd, t));
 #if RM_LAZY_CULL
-    bool tiny = false;
-    float d = scene_lazy<false>(q, t, lc, F.blend, F.omblend, dummy, tiny);
-    if (__builtin_expect(tiny, 0)) d = scene_impl<false, true>(q, F.blend, F.omblend, dummy, tiny);
+    const float d = scene_lazy(q, t, lc, F.blend, F.omblend);
 #else
     const float d = scene<false>(q, F.blend, F.omblend, dummy);
 #endif
@@ -56,7 +63,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   if (hit) {
     // the opU id (and colour) of the hit: the same sdf at the same point
     const f3 q = add(ro, muls(rd, t));
-    scene<true>(q, F.blend, F.omblend, id);
+    scene_exact<true>(q, F.blend, F.omblend, id);
     col = hit_color(id, q);
     return t;
   }

@@ -74,102 +74,43 @@ struct Frame {
 };
 
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
-// Minimum scene distance and the opU id (glsl:107-123).  `id` follows opU's
-// rule exactly: a later primitive replaces the running one unless the running
-// distance is strictly smaller.  blend/omblend carry mix()'s a and 1-a.
+// Three exact evaluations of the same sdf (value and opU id equal to a literal
+// transcription):
+//   scene_exact  — every primitive;
+//   scene_cull   — bounding-sphere culling (shadow march, normal probes, wave-queue);
+//   scene_lazy   — lazy culling along a march ray (RayMarch / reflectedRay loops).
+// opU (glsl:105): a later primitive replaces the running one unless the
+// running distance is strictly smaller, so ties go to the later primitive.
 //
-// SAFE = false uses the cheap exact sequences of rm_fastmath.hpp (sqrt_core,
-// div_capbb), each exact on its proven domain; any lane whose operands leave
-// that domain (a sqrt argument in (0, 2^-96), |capsule numerator| < 2^-100)
-// sets `tiny`, and scene() recomputes those lanes with SAFE = true (the full
-// correctly-rounded forms).  Either way the result is the IEEE value.
-template <bool WANT_ID, bool SAFE>
-__device__ __forceinline__ float scene_impl(f3 p, float blend, float omblend, int& id, bool& tiny) {
-  auto SQ = [](float x) { return SAFE ? sqrt_cr_nonneg(x) : sqrt_core(x); };
-  // sphere (15,0,-10) r3, id 0   glsl:111
-  const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
-  const float ay2 = ay * ay, az2 = az * az;
-  const float x0 = (ax * ax + ay2) + az2;
-  float d = SQ(x0) - 3.0f;
-  if (WANT_ID) id = 0;
-  // sphere (-25,0,-10) r3, id 1  glsl:112
-  const float bx = p.x + 25.0f;
-  const float x1 = (bx * bx + ay2) + az2;
-  const float d1 = SQ(x1) - 3.0f;
-  if (WANT_ID) id = (d < d1) ? id : 1;
-  d = fminf(d, d1);
-  // mix(box, sphere, blend) at (-5,0,-10), id 4   glsl:87-91,115-117
-  const float cx = p.x + 5.0f;
-  const float cx2 = cx * cx;
-  const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
-  const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
-  const float xb = (mx * mx + my * my) + mz * mz;
-  const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + SQ(xb);
-  const float xs = (cx2 + ay2) + az2;
-  const float sph = SQ(xs) - 3.0f;
-  const float d4 = box * omblend + sph * blend;
-  if (WANT_ID) id = (d < d4) ? id : 4;
-  d = fminf(d, d4);
-  // torus at (-5,0,10), (pos - c).xzy, t = (2.5, 0.5), id 5   glsl:93-96,119
-  const float tz = p.z - 10.0f;
-  const float xt1 = cx2 + ay2;
-  const float l = SQ(xt1) - 2.5f;
-  const float xt2 = l * l + tz * tz;
-  const float d5 = SQ(xt2) - 0.5f;
-  if (WANT_ID) id = (d < d5) ? id : 5;
-  d = fminf(d, d5);
-  // capsule at (-5,-2,-30), a(-.1,.1,-.1) b(2,4,2) r1, id 6   glsl:98-103,120
-  const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
-  const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
-  float h = SAFE ? hn / CAP_BB_HOST : div_capbb(hn);
-  h = fminf(fmaxf(h, 0.0f), 1.0f);
-  const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
-  const float xc = (ex * ex + ey * ey) + ez * ez;
-  const float d6 = SQ(xc) - 1.0f;
-  if (WANT_ID) id = (d < d6) ? id : 6;
-  d = fminf(d, d6);
-  // plane y = -5.5, id 7 (MATTE)   glsl:85,121
-  const float d7 = p.y + 5.5f;
-  if (WANT_ID) id = (d < d7) ? id : 7;
-  d = fminf(d, d7);
-  if (!SAFE) {
-    // operands outside the fast sequences' proven domains (see above)
-    const float m = fminf(fminf(fminf(x0, x1), fminf(xs, xt1)), fminf(xt2, xc));
-    tiny = (m < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN)) |
-           (fabsf(hn) < DIV_CAPBB_MIN);
-  }
-  return d;
-}
+// Square roots use sqrt_core (rm_fastmath.hpp): correctly rounded on {0} U
+// [2^-96, FLT_MAX] and < 2^-47 on (0, 2^-96) (both proven exhaustively).  Every
+// use but one subtracts R in {3, 2.5, 1, 0.5} right away, and RN(s - R) = -R for
+// every s < 2^-26, so the result is exact on the whole domain; the box's outer
+// length (used unshifted) takes the full-range sqrt_cr_nonneg.  The capsule
+// divide div_capbb is exact for |x| >= 2^-100; below that, h <= 2^-104 and
+// every BA*h term underflows out of (BA*h)^2 or is absorbed by a |pa| >= 2^-27,
+// so xc (hence the sdf) is identical.
+//
+// Culled primitives are strictly farther than the minimum, so the distance-only
+// variants return the running minimum over the plane and the evaluated
+// primitives directly (no merge needed).
 
-// ---- scene with exact bounding-sphere culling --------------------------------
-// Same value and id as scene_impl.  Each expensive primitive k gets a lower
-// bound LB_k <= its float sdf and the plane/spheres/blend give an upper bound
-// U >= the float minimum, from raw v_sqrt_f32 (within 1.5 ulp, see
-// rm_fastmath.hpp) widened by a relative 2^-12 and an absolute 2^-18 margin.
-// If LB_k > U the primitive is strictly farther than the minimum: it can
-// neither be the minimum nor tie it (opU ties go to the later primitive), so
-// skipping it changes nothing.  A primitive is evaluated exactly when any lane
-// of the wave needs it (the branch is skipped only when no lane does).
-//   bounding spheres (centre, radius):   sdf >= |p - c| - R   and, for U,
-//   sphere  (15,0,-10) / (-25,0,-10): R = 3 (exact: sdf = |p - c| - 3)
-//   box/sphere blend (-5,0,-10): R = |(3,2.5,2.5)| = 4.6368 (box circumradius);
-//                                upper bound |p - c| - 2.5 (box inradius)
-//   torus (-5,0,10): R = 2.5 + 0.5
-//   capsule: centre = midpoint of a..b = (-4.05,0.05,-29.05), R = |b-a|/2 + 1
+// Capsule and bounding-sphere constants.
 constexpr float CULL_REL_LO = 1.0f - 0x1p-12f;
 constexpr float CULL_REL_HI = 1.0f + 0x1p-12f;
 constexpr float CULL_ABS = 0x1p-18f;
-constexpr float R_BLEND_LO = 4.63682f;   // >= sqrt(3^2 + 2.5^2 + 2.5^2) = 4.636809
-constexpr float R_TORUS = 3.0f;
-constexpr float R_CAPSULE = 3.45115f;    // >= sqrt(24.03)/2 + 1 = 3.451050
-constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;
+constexpr float R_BLEND_LO = 4.63682f;   // >= |(3,2.5,2.5)| = 4.636809, box circumradius
+constexpr float R_TORUS = 3.0f;          // 2.5 + 0.5
+constexpr float R_CAPSULE = 3.45115f;    // >= |b-a|/2 + 1 = sqrt(24.03)/2 + 1 = 3.451050
+constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;  // segment midpoint
 
 #ifdef RM_STATS
 // Diagnostic build only: wave-level counts of exact primitive evaluations.
 __device__ unsigned long long g_stats[16];
 #define RM_STAT(k)                                                   \
   do {                                                               \
-    if (__lane_id() == __builtin_ffsll(__ballot(1)) - 1) atomicAdd(&g_stats[k], 1ull); \
+    const unsigned long long m_ = __ballot(1);                       \
+    if (__lane_id() == __builtin_ffsll(m_) - 1) atomicAdd(&g_stats[k], 1ull); \
   } while (0)
 #else
 #define RM_STAT(k) \
@@ -177,71 +118,58 @@ __device__ unsigned long long g_stats[16];
   } while (0)
 #endif
 
+// Exact per-primitive distances from shared centre offsets.
+struct Offs {
+  float ax, ay, az, bx, cx, ay2, az2, cx2;
+};
+__device__ __forceinline__ Offs offsets(f3 p) {
+  Offs o;
+  o.ax = p.x - 15.0f;  // sphere 0 centre (15,0,-10)
+  o.ay = p.y;
+  o.az = p.z + 10.0f;
+  o.bx = p.x + 25.0f;  // sphere 1 centre (-25,0,-10)
+  o.cx = p.x + 5.0f;   // blend (-5,0,-10), torus (-5,0,10), capsule (-5,-2,-30)
+  o.ay2 = o.ay * o.ay;
+  o.az2 = o.az * o.az;
+  o.cx2 = o.cx * o.cx;
+  return o;
+}
+__device__ __forceinline__ float sd_sphere0(const Offs& o, float x0) { return sqrt_core(x0) - 3.0f; }
+__device__ __forceinline__ float sd_blend(const Offs& o, float xs, float blend, float omblend) {
+  // mix(sdBox(q, (3,2.5,2.5)), sdSphere(q, 3), blend)   glsl:87-91,115-117
+  const float qx = fabsf(o.cx) - 3.0f, qy = fabsf(o.ay) - 2.5f, qz = fabsf(o.az) - 2.5f;
+  const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
+  const float xb = (mx * mx + my * my) + mz * mz;
+  const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + sqrt_cr_nonneg(xb);
+  const float sph = sqrt_core(xs) - 3.0f;
+  return box * omblend + sph * blend;
+}
+__device__ __forceinline__ float sd_torus(const Offs& o, float tz) {
+  // sdTorus((p - c).xzy, (2.5, 0.5))   glsl:93-96,119
+  const float l = sqrt_core(o.cx2 + o.ay2) - 2.5f;
+  return sqrt_core(l * l + tz * tz) - 0.5f;
+}
+__device__ __forceinline__ float sd_capsule(const Offs& o, f3 p) {
+  // sdCapsule(p - c, a, b, 1)   glsl:98-103,120
+  const float px_ = o.cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
+  const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
+  const float h = fminf(fmaxf(div_capbb(hn), 0.0f), 1.0f);
+  const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
+  return sqrt_core((ex * ex + ey * ey) + ez * ez) - 1.0f;
+}
+
 template <bool WANT_ID>
-__device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, int& id, bool& tiny) {
-  // centre offsets and squared centre distances (shared sub-terms)
-  const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
-  const float bx = p.x + 25.0f, cx = p.x + 5.0f, tz = p.z - 10.0f;
-  const float ay2 = ay * ay, az2 = az * az, cx2 = cx * cx;
-  const float x0 = (ax * ax + ay2) + az2;     // sphere 0 (exact sdf argument)
-  const float x1 = (bx * bx + ay2) + az2;     // sphere 1 (exact sdf argument)
-  const float xs = (cx2 + ay2) + az2;         // blend centre (= its sphere's argument)
-  const float xt1 = cx2 + ay2;                // torus inner argument
-  const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-  const float xtc = xt1 + tz * tz;            // torus centre (bound only)
-  const float xk = (kx * kx + ky * ky) + kz * kz;  // capsule centre (bound only)
-  const float r0 = __builtin_amdgcn_sqrtf(x0), r1 = __builtin_amdgcn_sqrtf(x1);
-  const float rs = __builtin_amdgcn_sqrtf(xs), rt = __builtin_amdgcn_sqrtf(xtc);
-  const float rk = __builtin_amdgcn_sqrtf(xk);
-  const float d7 = p.y + 5.5f;  // plane, exact (glsl:85,121)
-  // upper bound of the minimum
-  float U = fminf(d7, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
-  U = fminf(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f));
-  U = fminf(U, __builtin_fmaf(rs, CULL_REL_HI, CULL_ABS - 2.5f));
-  RM_STAT(0);
-  const float INF = __builtin_huge_valf();
-  float d0 = INF, d1 = INF, d4 = INF, d5 = INF, d6 = INF;
-  bool tn = false;
-  if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
-    RM_STAT(1);
-    d0 = sqrt_core(x0) - 3.0f;  // glsl:111
-    tn |= x0 < SQRT_CORE_MIN;
-  }
-  if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
-    RM_STAT(2);
-    d1 = sqrt_core(x1) - 3.0f;  // glsl:112
-    tn |= x1 < SQRT_CORE_MIN;
-  }
-  if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {  // glsl:87-91,115-117
-    RM_STAT(3);
-    const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
-    const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
-    const float xb = (mx * mx + my * my) + mz * mz;
-    const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + sqrt_core(xb);
-    const float sph = sqrt_core(xs) - 3.0f;
-    d4 = box * omblend + sph * blend;
-    tn |= (xs < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN));
-  }
-  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {  // glsl:93-96,119
-    RM_STAT(4);
-    const float l = sqrt_core(xt1) - 2.5f;
-    const float xt2 = l * l + tz * tz;
-    d5 = sqrt_core(xt2) - 0.5f;
-    tn |= (xt1 < SQRT_CORE_MIN) | (xt2 < SQRT_CORE_MIN);
-  }
-  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {  // glsl:98-103,120
-    RM_STAT(5);
-    const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
-    const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
-    const float h = fminf(fmaxf(div_capbb(hn), 0.0f), 1.0f);
-    const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
-    const float xc = (ex * ex + ey * ey) + ez * ez;
-    d6 = sqrt_core(xc) - 1.0f;
-    tn |= (xc < SQRT_CORE_MIN) | (fabsf(hn) < DIV_CAPBB_MIN);
-  }
-  tiny = tn;
-  // opU chain in the reference order (glsl:111-121); culled entries are +inf
-  float d = d0;
+__device__ __forceinline__ float scene_exact(f3 p, float blend, float omblend, int& id) {
+  const Offs o = offsets(p);
+  const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
+  const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
+  const float xs = (o.cx2 + o.ay2) + o.az2;
+  float d = sqrt_core(x0) - 3.0f;                           // glsl:111
+  const float d1 = sqrt_core(x1) - 3.0f;                    // glsl:112
+  const float d4 = sd_blend(o, xs, blend, omblend);          // glsl:115-117
+  const float d5 = sd_torus(o, p.z - 10.0f);                 // glsl:119
+  const float d6 = sd_capsule(o, p);                         // glsl:120
+  const float d7 = p.y + 5.5f;                               // glsl:85,121
   if (WANT_ID) {
     id = 0;
     id = (d < d1) ? id : 1;
@@ -254,30 +182,101 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
     d = vmin(d, d6);
     id = (d < d7) ? id : 7;
     d = vmin(d, d7);
-  } else {
-    d = vmin3(vmin3(d, d1, d4), vmin(d5, d6), d7);
+    return d;
   }
-  return d;
+  return vmin3(vmin3(d, d1, d4), vmin(d5, d6), d7);
 }
 
-// ---- scene with LAZY culling along a ray ----------------------------------------
-// For a march p(t) = ro + rd*t.  Primitive k is skipped while t < te[k].  When a
-// primitive is re-tested at p_i (t_i) with upper bound U_i >= min(p_i) and
-// lower bound LB_k(p_i) <= sdf_k(p_i), and LB_k > U_i, then for any later
-// point p_j on the ray, by the 1-Lipschitz property of the distances,
-//   sdf_k(p_j) - min(p_j) >= (LB_k - U_i) - 2 |p_j - p_i|,  |p_j - p_i| ~ |rd| (t_j - t_i),
-// so k stays strictly above the minimum (cannot be it, cannot tie it) while
-//   t_j < te_k = t_i + (LB_k - U_i - slack) / (2 |rd| (1 + 2^-10)).
-// `slack` covers the float error of the evaluated sdfs and of p(t) itself
-// (relative 2^-14 of |ro|_1 + |rd| t + 64 — generous against ~2^-21 actual).
-// A primitive whose bound does not cull it is evaluated exactly and re-tested
-// at the next step.  U_i = min(plane, exact values evaluated so far this
-// step).  The minimum and the opU id are merged in the reference order, so the
-// result equals scene_impl's.
+// Bounding-sphere culling.  Each expensive primitive k has a lower bound
+// LB_k <= its float sdf and the plane/spheres/blend give an upper bound
+// U >= the float minimum, from raw v_sqrt_f32 (within 1.5 ulp) widened by a
+// relative 2^-12 and an absolute 2^-18 margin:
+//   sdf >= |p - c| - R:  spheres R = 3 (exact), blend R = box circumradius,
+//   torus R = 3, capsule R = |b-a|/2 + 1 about the segment midpoint;
+//   U candidates: plane (exact), spheres |p-c| - 3, blend |p-c| - 2.5 (box inradius).
+// LB_k > U  =>  primitive k is strictly farther than the minimum: skip it.  The
+// branch for k runs when any lane of the wave needs it.
+template <bool WANT_ID>
+__device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, int& id) {
+  const Offs o = offsets(p);
+  const float tz = p.z - 10.0f;
+  const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
+  const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
+  const float xs = (o.cx2 + o.ay2) + o.az2;
+  const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
+  const float xtc = (o.cx2 + o.ay2) + tz * tz;
+  const float xk = (kx * kx + ky * ky) + kz * kz;
+  const float r0 = __builtin_amdgcn_sqrtf(x0), r1 = __builtin_amdgcn_sqrtf(x1);
+  const float rs = __builtin_amdgcn_sqrtf(xs), rt = __builtin_amdgcn_sqrtf(xtc);
+  const float rk = __builtin_amdgcn_sqrtf(xk);
+  const float d7 = p.y + 5.5f;
+  float U = vmin(d7, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
+  U = vmin3(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f),
+            __builtin_fmaf(rs, CULL_REL_HI, CULL_ABS - 2.5f));
+  RM_STAT(0);
+  if (WANT_ID) {
+    const float INF = __builtin_huge_valf();
+    float d0 = INF, d1 = INF, d4 = INF, d5 = INF, d6 = INF;
+    if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) d0 = sqrt_core(x0) - 3.0f;
+    if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) d1 = sqrt_core(x1) - 3.0f;
+    if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U)
+      d4 = sd_blend(o, xs, blend, omblend);
+    if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) d5 = sd_torus(o, tz);
+    if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) d6 = sd_capsule(o, p);
+    float d = d0;
+    id = 0;
+    id = (d < d1) ? id : 1;
+    d = vmin(d, d1);
+    id = (d < d4) ? id : 4;
+    d = vmin(d, d4);
+    id = (d < d5) ? id : 5;
+    d = vmin(d, d5);
+    id = (d < d6) ? id : 6;
+    d = vmin(d, d6);
+    id = (d < d7) ? id : 7;
+    d = vmin(d, d7);
+    return d;
+  }
+  float m = d7;  // running minimum over the plane and the evaluated primitives
+  if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    RM_STAT(1);
+    m = vmin(m, sqrt_core(x0) - 3.0f);
+  }
+  if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    RM_STAT(2);
+    m = vmin(m, sqrt_core(x1) - 3.0f);
+  }
+  if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {
+    RM_STAT(3);
+    m = vmin(m, sd_blend(o, xs, blend, omblend));
+  }
+  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {
+    RM_STAT(4);
+    m = vmin(m, sd_torus(o, tz));
+  }
+  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {
+    RM_STAT(5);
+    m = vmin(m, sd_capsule(o, p));
+  }
+  return m;
+}
+
+// ---- lazy culling along a ray ------------------------------------------------------
+// For a march p(t) = ro + rd*t.  Primitive k is skipped while t < te[k].  When k
+// is re-tested at p_i (t_i) with U_i >= min(p_i) and LB_k(p_i) > U_i, then for
+// any later point p_j of the ray, by the 1-Lipschitz property of distances,
+//   sdf_k(p_j) - min(p_j) >= (LB_k - U_i) - 2 |p_j - p_i|,   |p_j - p_i| ~ |rd| (t_j - t_i),
+// so k stays strictly above the minimum while
+//   t_j < te_k = t_i + (LB_k - U_i - slack) / (2 |rd|) * (1 - 2^-10).
+// `slack` covers the float error of the evaluated sdfs and of p(t) itself:
+// relative 2^-14 of |ro|_1 + |rd| t + 64 (the actual errors are ~2^-21).
+// U_i = min(plane, exact values of this step's evaluated primitives).  A
+// primitive whose bound does not cull it is evaluated exactly and re-tested at
+// the next step.  The distance returned is the running minimum.
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
-  float rdlen;   // |rd| (upper-rounded)
+  float rdlen;   // |rd| (rounded up)
   float ro1;     // |ro|_1
 };
 
@@ -290,105 +289,60 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
   c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
 }
 
-template <bool WANT_ID>
-__device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend, float omblend,
-                                            int& id, bool& tiny) {
-  const float INF = __builtin_huge_valf();
-  const float d7 = p.y + 5.5f;  // plane, exact (glsl:85,121)
-  float d0 = INF, d1 = INF, d4 = INF, d5 = INF, d6 = INF;
-  bool tn = false;
+__device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend,
+                                            float omblend) {
+  float m = p.y + 5.5f;  // plane, exact (glsl:85,121); running minimum
+  RM_STAT(8);
   if (t >= lc.temin) {
-    float U = d7;
+    RM_STAT(9);
     const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
     const float inv2v = 0.5f * (1.0f - 0x1p-10f) / lc.rdlen;
-    // expiry update: k stays culled while the ray travels (lb - U - slack)/2
-    auto retest = [&](float x, float R, float& te) -> bool {  // true: evaluate exactly
+    // re-test k; returns true when k must be evaluated exactly at this step
+    auto retest = [&](float x, float R, float& te) -> bool {
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
-      const float m = lb - U - slack;
-      if (m > 0.0f) {
-        te = __builtin_fmaf(m, inv2v, t);
-        return false;
-      }
-      te = t;
-      return true;
+      const float g = lb - m - slack;
+      te = (g > 0.0f) ? __builtin_fmaf(g, inv2v, t) : t;
+      return !(g > 0.0f);
     };
-    const float ax = p.x - 15.0f, ay = p.y, az = p.z + 10.0f;
-    const float ay2 = ay * ay, az2 = az * az;
-    const float cx = p.x + 5.0f, cx2 = cx * cx;
+    const Offs o = offsets(p);
     if (t >= lc.te[0]) {  // sphere (15,0,-10) r3, glsl:111
-      const float x0 = (ax * ax + ay2) + az2;
+      const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
       if (retest(x0, 3.0f, lc.te[0])) {
-        d0 = sqrt_core(x0) - 3.0f;
-        U = vmin(U, d0);
-        tn |= x0 < SQRT_CORE_MIN;
+        RM_STAT(10);
+        m = vmin(m, sqrt_core(x0) - 3.0f);
       }
     }
     if (t >= lc.te[1]) {  // sphere (-25,0,-10) r3, glsl:112
-      const float bx = p.x + 25.0f;
-      const float x1 = (bx * bx + ay2) + az2;
+      const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
       if (retest(x1, 3.0f, lc.te[1])) {
-        d1 = sqrt_core(x1) - 3.0f;
-        U = vmin(U, d1);
-        tn |= x1 < SQRT_CORE_MIN;
+        RM_STAT(11);
+        m = vmin(m, sqrt_core(x1) - 3.0f);
       }
     }
-    if (t >= lc.te[2]) {  // box/sphere blend, glsl:87-91,115-117
-      const float xs = (cx2 + ay2) + az2;
+    if (t >= lc.te[2]) {  // box/sphere blend, glsl:115-117
+      const float xs = (o.cx2 + o.ay2) + o.az2;
       if (retest(xs, R_BLEND_LO, lc.te[2])) {
-        const float qx = fabsf(cx) - 3.0f, qy = fabsf(ay) - 2.5f, qz = fabsf(az) - 2.5f;
-        const float mx = fmaxf(qx, 0.0f), my = fmaxf(qy, 0.0f), mz = fmaxf(qz, 0.0f);
-        const float xb = (mx * mx + my * my) + mz * mz;
-        const float box = fminf(fmaxf(qx, fmaxf(qy, qz)), 0.0f) + sqrt_core(xb);
-        const float sph = sqrt_core(xs) - 3.0f;
-        d4 = box * omblend + sph * blend;
-        U = vmin(U, d4);
-        tn |= (xs < SQRT_CORE_MIN) | ((xb > 0.0f) & (xb < SQRT_CORE_MIN));
+        RM_STAT(12);
+        m = vmin(m, sd_blend(o, xs, blend, omblend));
       }
     }
-    if (t >= lc.te[3]) {  // torus, glsl:93-96,119
+    if (t >= lc.te[3]) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      const float xt1 = cx2 + ay2;
-      if (retest(xt1 + tz * tz, R_TORUS, lc.te[3])) {
-        const float l = sqrt_core(xt1) - 2.5f;
-        const float xt2 = l * l + tz * tz;
-        d5 = sqrt_core(xt2) - 0.5f;
-        U = vmin(U, d5);
-        tn |= (xt1 < SQRT_CORE_MIN) | (xt2 < SQRT_CORE_MIN);
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3])) {
+        RM_STAT(13);
+        m = vmin(m, sd_torus(o, tz));
       }
     }
-    if (t >= lc.te[4]) {  // capsule, glsl:98-103,120
+    if (t >= lc.te[4]) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
       if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
-        const float px_ = cx - CAP_AX, py_ = (p.y + 2.0f) - CAP_AY, pz_ = (p.z + 30.0f) - CAP_AZ;
-        const float hn = (px_ * CAP_BAX + py_ * CAP_BAY) + pz_ * CAP_BAZ;
-        const float h = fminf(fmaxf(div_capbb(hn), 0.0f), 1.0f);
-        const float ex = px_ - CAP_BAX * h, ey = py_ - CAP_BAY * h, ez = pz_ - CAP_BAZ * h;
-        const float xc = (ex * ex + ey * ey) + ez * ez;
-        d6 = sqrt_core(xc) - 1.0f;
-        U = vmin(U, d6);
-        tn |= (xc < SQRT_CORE_MIN) | (fabsf(hn) < DIV_CAPBB_MIN);
+        RM_STAT(14);
+        m = vmin(m, sd_capsule(o, p));
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
   }
-  tiny = tn;
-  float d = d0;
-  if (WANT_ID) {
-    id = 0;
-    id = (d < d1) ? id : 1;
-    d = vmin(d, d1);
-    id = (d < d4) ? id : 4;
-    d = vmin(d, d4);
-    id = (d < d5) ? id : 5;
-    d = vmin(d, d5);
-    id = (d < d6) ? id : 6;
-    d = vmin(d, d6);
-    id = (d < d7) ? id : 7;
-    d = vmin(d, d7);
-  } else {
-    d = vmin3(vmin3(d, d1, d4), vmin(d5, d6), d7);
-  }
-  return d;
+  return m;
 }
 
 #ifndef RM_SCENE_CULL
@@ -397,11 +351,8 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
 
 template <bool WANT_ID>
 __device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id) {
-  bool tiny = false;
-  float d = RM_SCENE_CULL ? scene_cull<WANT_ID>(p, blend, omblend, id, tiny)
-                          : scene_impl<WANT_ID, false>(p, blend, omblend, id, tiny);
-  if (__builtin_expect(tiny, 0)) d = scene_impl<WANT_ID, true>(p, blend, omblend, id, tiny);
-  return d;
+  return RM_SCENE_CULL ? scene_cull<WANT_ID>(p, blend, omblend, id)
+                       : scene_exact<WANT_ID>(p, blend, omblend, id);
 }
 
 // softshadow's  res = min(res, k * h / t)  (glsl:211), exactly.  The quotient

@@ -32,12 +32,17 @@ __global__ void k_sqrt(unsigned long long* bad, unsigned* first) {
     float c0 = __builtin_amdgcn_sqrtf(x);  // raw v_sqrt_f32
     float c1 = rmd::sqrt_cr_nonneg(x);      // librm's exact sequence
     // sqrt_core: exact on {0} U [2^-96, FLT_MAX] (its documented domain)
+    float c2 = rmd::sqrt_core(x);
     if (x == 0.0f || x >= rmd::SQRT_CORE_MIN) {
-      float c2 = rmd::sqrt_core(x);
       if (__float_as_uint(c2) != __float_as_uint(ref)) {
         atomicAdd(&bad[2], 1ull);
         atomicMin(&first[2], (unsigned)i);
       }
+    } else if (!(c2 >= 0.0f && c2 < 0x1p-47f)) {
+      // below 2^-96 sqrt_core must stay in [0, 2^-47): then RN(s - R) = -R for
+      // every R in {3, 2.5, 1, 0.5} (rm_scene.hpp)
+      atomicAdd(&bad[3], 1ull);
+      atomicMin(&first[3], (unsigned)i);
     }
     if (__float_as_uint(c0) != __float_as_uint(ref)) {
       atomicAdd(&bad[0], 1ull);
@@ -67,6 +72,13 @@ __global__ void k_div(unsigned long long* bad, unsigned* first) {
       atomicMin(&first[reg], u & 0x7fffffffu);
       atomicMax(&first[2 + reg], u & 0x7fffffffu);
     }
+    if (fabsf(x) < 0x1p-100f) {
+      // below 2^-100 div_capbb need not be exact but must stay tiny and keep the
+      // sign: |q| <= 2^-104 and q*x >= 0 (rm_scene.hpp's capsule argument)
+      if (!(fabsf(c1) <= 0x1p-104f && !(c1 * x < 0.0f) && !(c1 > 0.0f && x < 0.0f) &&
+            !(c1 < 0.0f && x > 0.0f)))
+        atomicAdd(&bad[2], 1ull);
+    }
   }
 }
 
@@ -86,7 +98,8 @@ int main() {
   printf("sqrt  raw v_sqrt_f32 mismatches: %llu (first 0x%08x)\n", hb[0], hf[0]);
   printf("sqrt  sqrt_cr_nonneg mismatches: %llu (first 0x%08x)\n", hb[1], hf[1]);
   printf("sqrt  sqrt_core on {0}U[2^-96,max] mismatches: %llu (first 0x%08x)\n", hb[2], hf[2]);
-  const bool sqrt_ok = hb[1] == 0 && hb[2] == 0;
+  printf("sqrt  sqrt_core on (0,2^-96) outside [0,2^-47): %llu (first 0x%08x)\n", hb[3], hf[3]);
+  const bool sqrt_ok = hb[1] == 0 && hb[2] == 0 && hb[3] == 0;
   CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
   CK(hipMemset(first, 0xff, 2 * sizeof(unsigned)));
   CK(hipMemset(first + 2, 0, 2 * sizeof(unsigned)));
@@ -98,5 +111,6 @@ int main() {
          (double)CAP_BB, hb[0], hf[0], hf[2]);
   printf("div   x/CAP_BB div_capbb mismatches |x|>=2^-100: %llu (|x| bits 0x%08x..0x%08x)\n",
          hb[1], hf[1], hf[3]);
-  return (sqrt_ok && hb[1] == 0) ? 0 : 1;
+  printf("div   |x|<2^-100: results not tiny or sign-flipped: %llu\n", hb[2]);
+  return (sqrt_ok && hb[1] == 0 && hb[2] == 0) ? 0 : 1;
 }

@@ -7,6 +7,7 @@
 int main(int argc, char** argv) {
   int kernel = argc > 1 ? atoi(argv[1]) : RM_KERNEL_PIXEL;
   rm_config cfg = {3840, 2160, 0, RM_OUT_RGBA8, kernel, 0, 0, 0, 1};
+  rm_uniforms u0; (void)u0;
   rm_ctx* c; if (rm_create(&c, &cfg)) { printf("create failed %s\n", rm_last_error(nullptr)); return 1; }
   rm_uniforms u; rm_sweep_uniforms(30, 120, 3, 1, 0, &u); rm_set_uniforms(c, &u);
   unsigned long long z[16] = {0};
@@ -14,8 +15,12 @@ int main(int argc, char** argv) {
   rm_dispatch(c); rm_synchronize(c);
   unsigned long long h[16];
   hipMemcpyFromSymbol(h, HIP_SYMBOL(rmd::g_stats), sizeof h);
-  const char* nm[] = {"wave-sdf", "sphere0", "sphere1", "blend", "torus", "capsule"};
-  for (int k = 0; k < 6; ++k) printf("%-10s %12llu  %.3f\n", nm[k], h[k], (double)h[k] / h[0]);
+  const char* nm[] = {"cull-sdf", "sphere0", "sphere1", "blend", "torus", "capsule",
+                      "refl-iters", "lanes-in-march", "lazy-sdf", "lazy-block", "lz-sph0", "lz-sph1",
+                      "lz-blend", "lz-torus", "lz-capsule", "prim-iters"};
+  for (int k = 0; k < 16; ++k) printf("%-16s %12llu\n", nm[k], h[k]);
+  printf("march lane utilisation %.3f\n", (double)h[7] / (64.0 * (h[6] + h[15])));
+  printf("lazy block rate %.3f\n", (double)h[9] / h[8]);
   rm_destroy(c);
   return 0;
 }
