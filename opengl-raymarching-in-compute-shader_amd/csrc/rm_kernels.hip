@@ -75,6 +75,9 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 // GetNormal glsl:278-288
 template <bool COUNT>
 __device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c) {
+#ifdef RM_ABL_NO_NORMAL
+  return mk(0.0f, 1.0f, 0.0f);
+#endif
   int dummy;
   if (COUNT) c.normals++;
   float cc = scene<false>(pos, F.blend, F.omblend, dummy);
@@ -87,6 +90,9 @@ __device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c) {
 // softshadow glsl:201-216
 template <bool COUNT>
 __device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+#ifdef RM_ABL_NO_SHADOW
+  return 1.0f;
+#endif
   float res = 1.0f, t = 0.0f;
   int dummy;
   for (int i = 0; i < 16; ++i) {

@@ -239,23 +239,18 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   }
   float m = d7;  // running minimum over the plane and the evaluated primitives
   if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
-    RM_STAT(1);
     m = vmin(m, sqrt_core(x0) - 3.0f);
   }
   if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
-    RM_STAT(2);
     m = vmin(m, sqrt_core(x1) - 3.0f);
   }
   if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {
-    RM_STAT(3);
     m = vmin(m, sd_blend(o, xs, blend, omblend));
   }
   if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {
-    RM_STAT(4);
     m = vmin(m, sd_torus(o, tz));
   }
   if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {
-    RM_STAT(5);
     m = vmin(m, sd_capsule(o, p));
   }
   return m;
@@ -277,6 +272,7 @@ struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
   float rdlen;   // |rd| (rounded up)
+  float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float ro1;     // |ro|_1
 };
 
@@ -286,6 +282,7 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
   for (int k = 0; k < 5; ++k) c.te[k] = NEG;
   c.temin = NEG;
   c.rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);
+  c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(c.rdlen) * (1.0f - 0x1p-16f);
   c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
 }
 
@@ -296,9 +293,10 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
   if (t >= lc.temin) {
     RM_STAT(9);
     const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
-    const float inv2v = 0.5f * (1.0f - 0x1p-10f) / lc.rdlen;
+    const float inv2v = lc.inv2v;
     // re-test k; returns true when k must be evaluated exactly at this step
     auto retest = [&](float x, float R, float& te) -> bool {
+      RM_STAT(1);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       const float g = lb - m - slack;
       te = (g > 0.0f) ? __builtin_fmaf(g, inv2v, t) : t;
@@ -391,8 +389,24 @@ __device__ __forceinline__ f3 hit_color(int id, f3 p) {
   return id_color(id, id == 7 ? checkers(p) : 0.0f);
 }
 
+// pow(x, y) for x >= 0, y > 0, as GLSL specifies its precision: exp2(y * log2(x))
+// (GLSL 4.50 §8.2; the GL drivers the reference runs on evaluate it this way),
+// on the hardware transcendentals v_log_f32 / v_exp_f32.  pow(0, y) = 0.  Its
+// difference to a correctly rounded pow is a few float ulps (measured in
+// tests/test_gpu_parity.py); RM_POW_OCML selects ocml's powf instead.
+#ifndef RM_POW_OCML
+#define RM_POW_OCML 0
+#endif
+__device__ __forceinline__ float gpow(float x, float y) {
+  if (RM_POW_OCML) return powf(x, y);
+  return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+
 // getPointLight glsl:253-276
 __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f3 pos) {
+#ifdef RM_ABL_NO_LIGHT
+  return color;
+#endif
   f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
   f3 ambient = mk(F.lamb[0], F.lamb[1], F.lamb[2]);
   f3 viewDir = normalize(sub(pos, mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2])));
@@ -400,7 +414,7 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
   float NtoL = gmax(dot(normal, lightDir), 0.0f);
   f3 diffuse = muls(mk(F.ldif[0], F.ldif[1], F.ldif[2]), NtoL);
   f3 reflectDir = reflect(lightDir, normal);
-  float spec = powf(gmax(dot(viewDir, reflectDir), 0.0f), 32.0f);
+  float spec = gpow(gmax(dot(viewDir, reflectDir), 0.0f), 32.0f);
   f3 specular = muls(mk(F.lspec[0], F.lspec[1], F.lspec[2]), spec);
   float distance = len(sub(lpos, pos));
   float attenuation = 1.0f / ((F.lconst + F.llin * distance) + F.lquad * (distance * distance));
@@ -411,7 +425,10 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
 }
 
 __device__ __forceinline__ f3 gamma(f3 c) {
-  return mk(powf(c.x, 0.4545f), powf(c.y, 0.4545f), powf(c.z, 0.4545f));
+#ifdef RM_ABL_NO_GAMMA
+  return c;
+#endif
+  return mk(gpow(c.x, 0.4545f), gpow(c.y, 0.4545f), gpow(c.z, 0.4545f));
 }
 
 // castRay glsl:68-74 over vec4 (w included, as the GLSL does).

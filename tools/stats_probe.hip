@@ -15,7 +15,7 @@ int main(int argc, char** argv) {
   rm_dispatch(c); rm_synchronize(c);
   unsigned long long h[16];
   hipMemcpyFromSymbol(h, HIP_SYMBOL(rmd::g_stats), sizeof h);
-  const char* nm[] = {"cull-sdf", "sphere0", "sphere1", "blend", "torus", "capsule",
+  const char* nm[] = {"cull-sdf(shadow+normal)", "lazy-retests", "shadow-steps", "normal-calls", "-", "-",
                       "refl-iters", "lanes-in-march", "lazy-sdf", "lazy-block", "lz-sph0", "lz-sph1",
                       "lz-blend", "lz-torus", "lz-capsule", "prim-iters"};
   for (int k = 0; k < 16; ++k) printf("%-16s %12llu\n", nm[k], h[k]);
