@@ -103,6 +103,9 @@ def main() -> int:
                     help="pixel = k_pixel (RM_KERNEL_AUTO's choice), wavequeue = k_wavequeue")
     ap.add_argument("--row-block", type=int, default=8,
                     help="rows per interleaved block when sharding over ranks")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1: replay the frame from a captured hipGraph (rm_graph_dispatch); "
+                         "default: on for config 5 (BASELINE 'hipGraph-captured frame')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=4,
                     help="cpu_baseline renders every k-th row of one frame")
@@ -125,7 +128,15 @@ def main() -> int:
     cfg = CONFIGS[args.config]
     W, H = cfg["width"], cfg["height"]
     kernel = rm.RM_KERNEL_WAVEQUEUE if args.kernel == "wavequeue" else rm.RM_KERNEL_PIXEL
-    stream = torch.cuda.current_stream()
+    use_graph = (args.graph == 1) or (args.graph < 0 and args.config == 5)
+    if use_graph and kernel == rm.RM_KERNEL_WAVEQUEUE:
+        print("bench.py: --graph renders with the default kernel", file=sys.stderr)
+        return 2
+    # An explicit stream (torch's default stream has a NULL handle, which librm
+    # would replace by its own stream): librm's kernels and the RCCL gather are
+    # then ordered on one stream.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
 
     def uniforms(f):
         return rm.sweep_uniforms(f % SWEEP_FRAMES, SWEEP_FRAMES, cfg["bounces"], cfg["aa"],
@@ -146,9 +157,14 @@ def main() -> int:
         frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
         r.set_output_rgba8(frame.data_ptr())
     r.set_stream(stream.cuda_stream)
+    if use_graph:
+        r.graph_enable(True)
 
     def step(f):
-        r.dispatch(uniforms(f))
+        if use_graph:
+            r.graph_dispatch(uniforms(f))
+        else:
+            r.dispatch(uniforms(f))
         if ws > 1:
             glist = list(gathered.unbind(0)) if rank == 0 else None
             dist.gather(shard_buf, gather_list=glist, dst=0)
@@ -248,7 +264,7 @@ def main() -> int:
             "config": {"workload": f"cfg{args.config}: {cfg['desc']}", "width": W, "height": H,
                        "bounces": cfg["bounces"], "aa": cfg["aa"],
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
-                       "kernel": kname,
+                       "kernel": kname, "hipgraph": bool(use_graph),
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        if ws > 1 else "single GPU")},
             "fps": round(frames / elapsed, 3),

@@ -170,6 +170,17 @@ int rm_get_wave_iterations(rm_ctx *ctx, uint64_t *iters);
  * pixel's samples, reference units (requires cfg.counters). */
 int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
 
+/* ---- hipGraph frame replay (BASELINE cfg 5) ------------------------------ */
+/* rm_graph_enable(ctx, 1) switches the context to graph replay: the first
+ * rm_graph_dispatch captures [copy of the frame constants from pinned host
+ * memory to the device; render kernel reading them] into two double-buffered
+ * graph instances; every later rm_graph_dispatch writes the current uniforms
+ * to pinned memory and replays a graph on the context's stream (re-captured
+ * only when AA toggles, which changes the grid).  Same image as rm_dispatch.
+ * Not available with cfg.counters or RM_KERNEL_WAVEQUEUE. */
+int rm_graph_enable(rm_ctx *ctx, int enable);
+int rm_graph_dispatch(rm_ctx *ctx);
+
 /* ---- device-side interop (plain pointers; for stream/collective plumbing) - */
 /* Use an external stream (hipStream_t passed as void*); NULL = own stream. */
 int rm_set_stream(rm_ctx *ctx, void *hip_stream);

@@ -24,7 +24,18 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s);
+hipError_t launch_pixel_dev(const rmd::Frame& F, const rmd::Frame* dF, hipStream_t s);
 }  // namespace rm
+
+// One double-buffer slot of the graph path: pinned host + device frame
+// constants and the instantiated graph that copies and renders them.
+struct rm_graph_slot {
+  rmd::Frame* h = nullptr;
+  rmd::Frame* d = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipEvent_t done = nullptr;
+  bool used = false;
+};
 
 struct rm_ctx {
   rm_config cfg{};
@@ -46,6 +57,10 @@ struct rm_ctx {
   size_t ev_used = 0;
   double total_ms = 0.0;
   int64_t launches = 0;
+  bool graph_on = false;
+  int graph_aa = -1;  // AA value the graphs were captured for (grid shape depends on it)
+  int graph_next = 0;
+  rm_graph_slot gs[2];
   std::string err;
 };
 
@@ -113,7 +128,20 @@ rmd::Frame make_frame(const rm_ctx* c) {
   return F;
 }
 
+void graph_release(rm_ctx* c) {
+  for (auto& g : c->gs) {
+    if (g.done) (void)hipEventSynchronize(g.done);
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (g.done) (void)hipEventDestroy(g.done);
+    if (g.h) (void)hipHostFree(g.h);
+    if (g.d) (void)hipFree(g.d);
+    g = rm_graph_slot();
+  }
+  c->graph_aa = -1;
+}
+
 void free_all(rm_ctx* c) {
+  graph_release(c);
   if (c->d_rgba8) (void)hipFree(c->d_rgba8);
   if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
   if (c->d_counts) (void)hipFree(c->d_counts);
@@ -427,6 +455,104 @@ int rm_read_sdf_counts(rm_ctx* c, uint32_t* dst) {
   if (rc != RM_OK) return rc;
   RM_HIP(c, hipStreamSynchronize(c->stream));
   RM_HIP(c, hipMemcpy(dst, c->d_counts, (size_t)c->rows * c->cfg.width * 4, hipMemcpyDeviceToHost));
+  return RM_OK;
+}
+
+// ---- hipGraph frame replay -----------------------------------------------------------
+// Captures (once per AA setting) [H2D copy of the frame constants from pinned
+// host memory -> device, render kernel reading them] into two graph instances
+// with their own constant buffers, so the host can fill frame f+1's constants
+// while frame f renders.  rm_graph_dispatch replays one; nothing is captured per
+// frame.  Counters and the wave-queue kernel are not available on this path.
+static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
+  graph_release(c);
+  hipStream_t cs = nullptr;
+  RM_HIP(c, hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  int rc = RM_OK;
+  for (auto& g : c->gs) {
+    hipError_t e;
+    if ((e = hipHostMalloc(&g.h, sizeof(rmd::Frame), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMalloc(&g.d, sizeof(rmd::Frame))) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&g.done, hipEventDisableTiming)) != hipSuccess) {
+      rc = hip_fail(c, e, "graph buffers");
+      break;
+    }
+    *g.h = F;
+    hipGraph_t graph = nullptr;
+    if ((e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal)) != hipSuccess) {
+      rc = hip_fail(c, e, "hipStreamBeginCapture");
+      break;
+    }
+    hipError_t e1 = hipMemcpyAsync(g.d, g.h, sizeof(rmd::Frame), hipMemcpyHostToDevice, cs);
+    hipError_t e2 = rm::launch_pixel_dev(F, g.d, cs);
+    e = hipStreamEndCapture(cs, &graph);
+    if (e1 != hipSuccess || e2 != hipSuccess || e != hipSuccess) {
+      rc = hip_fail(c, e1 != hipSuccess ? e1 : (e2 != hipSuccess ? e2 : e), "graph capture");
+      if (graph) (void)hipGraphDestroy(graph);
+      break;
+    }
+    e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+      rc = hip_fail(c, e, "hipGraphInstantiate");
+      break;
+    }
+  }
+  (void)hipStreamDestroy(cs);
+  if (rc != RM_OK) {
+    graph_release(c);
+    return rc;
+  }
+  c->graph_aa = F.aa;
+  c->graph_next = 0;
+  return RM_OK;
+}
+
+int rm_graph_enable(rm_ctx* c, int enable) {
+  if (!c) return RM_ERR_INVALID;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if (!enable) {
+    graph_release(c);
+    c->graph_on = false;
+    return RM_OK;
+  }
+  if (c->cfg.counters) return fail(c, RM_ERR_STATE, "graph path does not collect counters");
+  if (c->cfg.kernel == RM_KERNEL_WAVEQUEUE)
+    return fail(c, RM_ERR_STATE, "graph path renders with the default kernel");
+  c->graph_on = true;
+  return RM_OK;
+}
+
+int rm_graph_dispatch(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  if (!c->graph_on) return fail(c, RM_ERR_STATE, "rm_graph_enable(ctx, 1) first");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  const rmd::Frame F = make_frame(c);
+  if (F.aa != c->graph_aa && (rc = graph_capture(c, F)) != RM_OK) return rc;
+  rm_graph_slot& g = c->gs[c->graph_next];
+  c->graph_next ^= 1;
+  if (g.used) RM_HIP(c, hipEventSynchronize(g.done));  // its constants were consumed
+  *g.h = F;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    if (c->ev_used == c->ev_pool.size()) {
+      std::pair<hipEvent_t, hipEvent_t> p;
+      RM_HIP(c, hipEventCreate(&p.first));
+      RM_HIP(c, hipEventCreate(&p.second));
+      c->ev_pool.push_back(p);
+    }
+    e0 = c->ev_pool[c->ev_used].first;
+    e1 = c->ev_pool[c->ev_used].second;
+    c->ev_used++;
+  }
+  if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
+  RM_HIP(c, hipGraphLaunch(g.exec, c->stream));
+  if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
+  RM_HIP(c, hipEventRecord(g.done, c->stream));
+  g.used = true;
+  c->dispatched = true;
   return RM_OK;
 }
 

@@ -168,10 +168,13 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 // are spatially coherent (similar step counts, same culled primitives).
 constexpr int kTile = 16;
 #ifndef RM_PIXEL_MIN_WAVES
-#define RM_PIXEL_MIN_WAVES 6
+#define RM_PIXEL_MIN_WAVES 5
+#endif
+#ifndef RM_SAMPLE_MIN_WAVES
+#define RM_SAMPLE_MIN_WAVES 6
 #endif
 template <bool COUNT>
-__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
+__device__ __forceinline__ void pixel_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int px = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
   const int lrow = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
 // lane shuffles before the /4 (glsl:315-335).
 constexpr int kSampleTile = 8;  // 8x8 pixels per 256-thread workgroup
 template <bool COUNT>
-__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_sample(Frame F) {
+__device__ __forceinline__ void sample_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
   const int px = blockIdx.x * kSampleTile + (wave & 1) * 4 + (q & 3);
@@ -282,6 +285,26 @@ __global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_sample(Frame F) {
   if (COUNT) F.sdf_counts[idx] = cnt;
 }
 
+// Entry points: frame constants by value (kernel arguments, rm_dispatch) or
+// through a device pointer (graph replay, rm_graph_dispatch: the graph copies
+// the per-frame constants from pinned host memory before the launch).
+template <bool COUNT>
+__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
+  pixel_body<COUNT>(F);
+}
+__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel_dev(const Frame* __restrict__ pF) {
+  const Frame F = *pF;
+  pixel_body<false>(F);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
+  sample_body<COUNT>(F);
+}
+__global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample_dev(const Frame* __restrict__ pF) {
+  const Frame F = *pF;
+  sample_body<false>(F);
+}
+
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
@@ -318,6 +341,19 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
     hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(256), 0, s, F);
   else
     hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(256), 0, s, F);
+  return hipGetLastError();
+}
+
+// Graph-path launch: frame constants read from device memory (no counters).
+hipError_t launch_pixel_dev(const rmd::Frame& F, const rmd::Frame* dF, hipStream_t s) {
+  if (F.aa) {
+    const dim3 g((F.width + rmd::kSampleTile - 1) / rmd::kSampleTile,
+                 (F.rows + rmd::kSampleTile - 1) / rmd::kSampleTile);
+    hipLaunchKernelGGL(rmd::k_sample_dev, g, dim3(256), 0, s, dF);
+  } else {
+    const dim3 g((F.width + rmd::kTile - 1) / rmd::kTile, (F.rows + rmd::kTile - 1) / rmd::kTile);
+    hipLaunchKernelGGL(rmd::k_pixel_dev, g, dim3(256), 0, s, dF);
+  }
   return hipGetLastError();
 }
 

@@ -115,6 +115,8 @@ _SIGS = {
     "rm_get_counters": (C.c_int, [_P, C.POINTER(rm_counters)]),
     "rm_read_sdf_counts": (C.c_int, [_P, _P]),
     "rm_get_wave_iterations": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "rm_graph_enable": (C.c_int, [_P, C.c_int]),
+    "rm_graph_dispatch": (C.c_int, [_P]),
     "rm_set_stream": (C.c_int, [_P, _P]),
     "rm_set_output_rgba8": (C.c_int, [_P, _P]),
     "rm_get_output_rgba8": (C.c_int, [_P, C.POINTER(_P)]),
@@ -327,6 +329,16 @@ class Renderer:
         if u is not None:
             self.set_uniforms(u)
         _check(lib().rm_dispatch(self._h), self._h)
+
+    def graph_enable(self, on: bool = True) -> None:
+        """Switch to hipGraph replay of the frame (BASELINE cfg 5)."""
+        _check(lib().rm_graph_enable(self._h, int(on)), self._h)
+
+    def graph_dispatch(self, u: Optional[rm_uniforms] = None) -> None:
+        """rm_dispatch through the captured graph (asynchronous)."""
+        if u is not None:
+            self.set_uniforms(u)
+        _check(lib().rm_graph_dispatch(self._h), self._h)
 
     def synchronize(self) -> None:
         """glMemoryBarrier (main.cpp:125) + wait."""

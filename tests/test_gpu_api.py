@@ -204,3 +204,38 @@ def test_full_size_rows_match_oracle_sample(rm, oracle, gpu):
     ref = oracle.render(u, W, H, rows=rows)
     np.testing.assert_array_equal(sc[rows], ref["sdf_counts"])
     assert np.abs(img[rows].astype(int) - ref["rgba8"].astype(int)).max() <= 1
+
+
+def test_graph_replay_matches_dispatch(rm, gpu):
+    """hipGraph frame replay (cfg 5 path): an animated sweep replayed from two
+    captured graphs equals plain dispatches frame for frame, including an AA
+    toggle (re-capture) and an external output buffer."""
+    import torch
+    W, H = 160, 90
+    frames = [(f, b, aa) for f, b, aa in [(0, 3, True), (1, 3, True), (2, 3, True), (3, 1, False),
+                                          (4, 1, False), (5, 3, True)]]
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    with rm.Renderer(W, H, outputs=3) as g, rm.Renderer(W, H, outputs=3) as r:
+        g.graph_enable(True)
+        for f, b, aa in frames:
+            u = rm.sweep_uniforms(f, 120, b, aa, 0)
+            r.dispatch(u)
+            g.graph_dispatch(u)
+            np.testing.assert_array_equal(g.read_rgba32f(), r.read_rgba32f())
+        g.set_output_rgba8(out.data_ptr())
+        u = rm.sweep_uniforms(9, 120, 3, True, 0)
+        g.graph_dispatch(u)
+        g.synchronize()
+        r.dispatch(u)
+        np.testing.assert_array_equal(out.cpu().numpy(), r.read_rgba8())
+        g.enable_timing(True)
+        for f in range(4):
+            g.graph_dispatch(rm.sweep_uniforms(f, 120, 3, True, 0))
+        ms, n = g.kernel_time_ms(reset=True)
+        assert n == 4 and ms > 0
+
+
+def test_graph_refuses_counters(rm, gpu):
+    with rm.Renderer(32, 32, counters=True) as r:
+        with pytest.raises(rm.RMError):
+            r.graph_enable(True)
