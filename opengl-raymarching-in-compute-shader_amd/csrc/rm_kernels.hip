@@ -27,13 +27,14 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   float t = 0.0f;
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
-  int dummy;
   bool hit = false;
 #if RM_LAZY_CULL
   LazyCull lc;
   lazy_init(lc, ro, rd);
 #endif
-  for (int i = 0; i < nmax; ++i) {
+  // One exit per step (hit | escape | step cap), tested with VALU: a single
+  // exec-mask update per iteration instead of one per GLSL break.
+  for (int i = 1;; ++i) {
 #ifdef RM_STATS
     {
       const unsigned long long m = __ballot(1);
@@ -47,17 +48,15 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #if RM_LAZY_CULL
     const float d = scene_lazy(q, t, lc, F.blend, F.omblend);
 #else
+    int dummy;
     const float d = scene<false>(q, F.blend, F.omblend, dummy);
 #endif
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
     }
-    if (d < 0.000001f * t) {
-      hit = true;
-      break;
-    }
-    if (d > tmax) break;
+    hit = d < 0.000001f * t;
+    if (hit | (d > tmax) | (i >= nmax)) break;
     t += d;
   }
   if (hit) {
@@ -171,7 +170,7 @@ constexpr int kTile = 16;
 #define RM_PIXEL_MIN_WAVES 5
 #endif
 #ifndef RM_SAMPLE_MIN_WAVES
-#define RM_SAMPLE_MIN_WAVES 6
+#define RM_SAMPLE_MIN_WAVES 8
 #endif
 template <bool COUNT>
 __device__ __forceinline__ void pixel_body(const Frame& F) {

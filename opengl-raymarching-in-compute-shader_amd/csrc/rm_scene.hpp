@@ -105,12 +105,16 @@ constexpr float R_CAPSULE = 3.45115f;    // >= |b-a|/2 + 1 = sqrt(24.03)/2 + 1 =
 constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;  // segment midpoint
 
 #ifdef RM_STATS
-// Diagnostic build only: wave-level counts of exact primitive evaluations.
-__device__ unsigned long long g_stats[16];
+// Diagnostic build only: g_stats[k] counts waves reaching point k, g_stats[16+k]
+// the active lanes there.
+__device__ unsigned long long g_stats[32];
 #define RM_STAT(k)                                                   \
   do {                                                               \
     const unsigned long long m_ = __ballot(1);                       \
-    if (__lane_id() == __builtin_ffsll(m_) - 1) atomicAdd(&g_stats[k], 1ull); \
+    if (__lane_id() == __builtin_ffsll(m_) - 1) {                    \
+      atomicAdd(&g_stats[k], 1ull);                                  \
+      atomicAdd(&g_stats[16 + (k)], (unsigned long long)__popcll(m_)); \
+    }                                                                \
   } while (0)
 #else
 #define RM_STAT(k) \
@@ -268,11 +272,18 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
 // U_i = min(plane, exact values of this step's evaluated primitives).  A
 // primitive whose bound does not cull it is evaluated exactly and re-tested at
 // the next step.  The distance returned is the running minimum.
+// Second, often longer budget: the plane distance is linear along the ray,
+// plane(p_j) = plane(p_i) + rd.y (t_j - t_i), and min(p_j) <= plane(p_j), so k
+// also stays above the minimum while
+//   t_j < t_i + (LB_k - plane(p_i) - slack) / (|rd| + rd.y) * (1 - 2^-10)
+// (|rd| + rd.y >= 0; level and downward rays get 2x and more).  te_k is the
+// later of the two expiries; both are valid, so their max is.
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
   float rdlen;   // |rd| (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
+  float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
   float ro1;     // |ro|_1
 };
 
@@ -283,55 +294,83 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
   c.temin = NEG;
   c.rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);
   c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(c.rdlen) * (1.0f - 0x1p-16f);
+  // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
+  // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
+  c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(c.rdlen + rd.y) * (1.0f - 0x1p-16f);
   c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
 }
+
+// RM_LAZY_WAVE: the block and each re-test are entered per wave (any lane
+// expired) and every active lane re-tests: lanes whose te has not expired keep
+// max(te, new te) -- both expiries are valid -- so the idle lanes of a
+// divergent re-test extend their budgets for free.
+#ifndef RM_LAZY_WAVE
+#define RM_LAZY_WAVE 1
+#endif
+#ifndef RM_LAZY_ALL
+#define RM_LAZY_ALL 0
+#endif
+#if RM_LAZY_ALL
+#define RM_LZ_ANY(c) true
+#define RM_LZ_BLOCK(c) __any(c)
+#elif RM_LAZY_WAVE
+#define RM_LZ_ANY(c) __any(c)
+#define RM_LZ_BLOCK(c) __any(c)
+#else
+#define RM_LZ_ANY(c) (c)
+#define RM_LZ_BLOCK(c) (c)
+#endif
 
 __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend,
                                             float omblend) {
   float m = p.y + 5.5f;  // plane, exact (glsl:85,121); running minimum
   RM_STAT(8);
-  if (t >= lc.temin) {
+  if (RM_LZ_BLOCK(t >= lc.temin)) {
     RM_STAT(9);
     const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
-    const float inv2v = lc.inv2v;
+    const float inv2v = lc.inv2v, invp = lc.invp;
+    const float pl = m + slack;  // plane(p_i) + slack
     // re-test k; returns true when k must be evaluated exactly at this step
     auto retest = [&](float x, float R, float& te) -> bool {
       RM_STAT(1);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       const float g = lb - m - slack;
-      te = (g > 0.0f) ? __builtin_fmaf(g, inv2v, t) : t;
-      return !(g > 0.0f);
+      const float bud = __builtin_fmaxf(g * inv2v, (lb - pl) * invp);
+      const float tn = (g > 0.0f) ? t + bud : t;
+      const bool expired = t >= te;
+      te = expired ? tn : __builtin_fmaxf(te, tn);
+      return expired & !(g > 0.0f);
     };
     const Offs o = offsets(p);
-    if (t >= lc.te[0]) {  // sphere (15,0,-10) r3, glsl:111
+    if (RM_LZ_ANY(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
       if (retest(x0, 3.0f, lc.te[0])) {
         RM_STAT(10);
         m = vmin(m, sqrt_core(x0) - 3.0f);
       }
     }
-    if (t >= lc.te[1]) {  // sphere (-25,0,-10) r3, glsl:112
+    if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
       if (retest(x1, 3.0f, lc.te[1])) {
         RM_STAT(11);
         m = vmin(m, sqrt_core(x1) - 3.0f);
       }
     }
-    if (t >= lc.te[2]) {  // box/sphere blend, glsl:115-117
+    if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
       if (retest(xs, R_BLEND_LO, lc.te[2])) {
         RM_STAT(12);
         m = vmin(m, sd_blend(o, xs, blend, omblend));
       }
     }
-    if (t >= lc.te[3]) {  // torus, glsl:119
+    if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
       if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3])) {
         RM_STAT(13);
         m = vmin(m, sd_torus(o, tz));
       }
     }
-    if (t >= lc.te[4]) {  // capsule, glsl:120
+    if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
       if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
         RM_STAT(14);

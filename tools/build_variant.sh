@@ -1,0 +1,23 @@
+#!/bin/bash
+# Build a librm variant with extra -D flags for A/B timing (tools/probe_variants.sh).
+#   tools/build_variant.sh NAME [-DFOO=1 ...]   -> tools/variants/librm_NAME.so
+#   tools/build_variant.sh NAME --rev GITREV    -> librm built from a committed revision
+set -e
+name=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/tools/variants; mkdir -p "$out"
+src=$root
+if [ "$1" = "--rev" ]; then
+  src=$(mktemp -d); git -C "$root" archive "$2" | tar -x -C "$src"; shift 2
+fi
+pkg=opengl-raymarching-in-compute-shader_amd
+flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$src/include $*"
+b=$(mktemp -d)
+for f in rm_api rm_kernels rm_wavequeue; do
+  /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/$f.hip" -o "$b/$f.o" &
+done
+/opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o
+rm -rf "$b"; [ "$src" != "$root" ] && rm -rf "$src"
+echo "$out/librm_$name.so"

@@ -10,17 +10,19 @@ int main(int argc, char** argv) {
   rm_uniforms u0; (void)u0;
   rm_ctx* c; if (rm_create(&c, &cfg)) { printf("create failed %s\n", rm_last_error(nullptr)); return 1; }
   rm_uniforms u; rm_sweep_uniforms(30, 120, 3, 1, 0, &u); rm_set_uniforms(c, &u);
-  unsigned long long z[16] = {0};
+  unsigned long long z[32] = {0};
   hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_stats), z, sizeof z);
   rm_dispatch(c); rm_synchronize(c);
-  unsigned long long h[16];
+  unsigned long long h[32];
   hipMemcpyFromSymbol(h, HIP_SYMBOL(rmd::g_stats), sizeof h);
   const char* nm[] = {"cull-sdf(shadow+normal)", "lazy-retests", "shadow-steps", "normal-calls", "-", "-",
                       "refl-iters", "lanes-in-march", "lazy-sdf", "lazy-block", "lz-sph0", "lz-sph1",
                       "lz-blend", "lz-torus", "lz-capsule", "prim-iters"};
-  for (int k = 0; k < 16; ++k) printf("%-16s %12llu\n", nm[k], h[k]);
+  printf("%-24s %12s %14s %6s\n", "point", "waves", "lanes", "lanes/wave");
+  for (int k = 0; k < 16; ++k)
+    printf("%-24s %12llu %14llu %6.1f\n", nm[k], h[k], h[16 + k], h[k] ? (double)h[16 + k] / h[k] : 0.0);
   printf("march lane utilisation %.3f\n", (double)h[7] / (64.0 * (h[6] + h[15])));
-  printf("lazy block rate %.3f\n", (double)h[9] / h[8]);
+  printf("lazy block rate: waves %.3f lanes %.3f\n", (double)h[9] / h[8], (double)h[25] / h[24]);
   rm_destroy(c);
   return 0;
 }
