@@ -14,6 +14,9 @@
 #ifndef RM_LAZY_CULL
 #define RM_LAZY_CULL 1
 #endif
+#ifndef RM_SHADOW_EXIT
+#define RM_SHADOW_EXIT 1
+#endif
 
 namespace rmd {
 
@@ -94,8 +97,14 @@ __device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 #endif
   float res = 1.0f, t = 0.0f;
   int dummy;
+  const ShadowExit ex = shadow_exit_init(F.k, ro, rd);
   for (int i = 0; i < 16; ++i) {
+    if (RM_SHADOW_EXIT && shadow_exit(ex, t)) {  // the remaining steps are no-ops
+      if (COUNT) c.shadow += 16 - i;
+      return res;
+    }
     float h = scene<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
+    RM_STAT(2);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
     res = shadow_min(res, F.k, h, t);

@@ -32,6 +32,10 @@
 
 #include "rm_scene.hpp"
 
+#ifndef RM_SHADOW_EXIT
+#define RM_SHADOW_EXIT 1
+#endif
+
 namespace rmd {
 
 enum : int { PH_IDLE = 0, PH_PEND = 1, PH_MARCH = 2, PH_NORMAL = 3, PH_SHADOW = 4 };
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
   int hid = -1;                        // id of the current hit (-1 = miss)
   float hchk = 0.f;                    // checkers() at the current hit point
   float res = 1.f;                     // softshadow running minimum
+  ShadowExit sx = {0.f, 0.f, 0.f, 0.f};  // softshadow early-exit bounds (rm_scene.hpp)
   uint32_t c_pix = 0;
   uint32_t c_rays = 0, c_march = 0, c_refl = 0, c_shadow = 0, c_norm = 0, c_light = 0;
   uint32_t c_iters = 0;
@@ -129,6 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
               t = 0.f;
               i = 0;
               res = 1.f;
+              sx = shadow_exit_init(F.k, ro, rd);
               phase = PH_SHADOW;
             } else if (F.bounces > 0) {
               pcol = hc;  // prevColor = primaryObject.color (glsl:167)
@@ -162,6 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
             t = 0.f;
             i = 0;
             res = 1.f;
+            sx = shadow_exit_init(F.k, ro, rd);
             phase = PH_SHADOW;
           } else {
             col = add(col, term);
@@ -323,6 +330,13 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
         t += d;
         ++i;
         done = (i >= 16);
+        if (!done && RM_SHADOW_EXIT && shadow_exit(sx, t)) {  // the remaining steps are no-ops
+          if (COUNT) {
+            c_shadow += 16 - i;
+            c_pix += 16 - i;
+          }
+          done = true;
+        }
       }
       if (done) {
         phase = PH_PEND;
