@@ -17,6 +17,9 @@
 #ifndef RM_SHADOW_EXIT
 #define RM_SHADOW_EXIT 1
 #endif
+#ifndef RM_MISS_EXIT
+#define RM_MISS_EXIT 1
+#endif
 
 namespace rmd {
 
@@ -35,8 +38,13 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   LazyCull lc;
   lazy_init(lc, ro, rd);
 #endif
-  // One exit per step (hit | escape | step cap), tested with VALU: a single
-  // exec-mask update per iteration instead of one per GLSL break.
+  // provable miss (rm_scene.hpp "early exits"): production stops there; the
+  // counting build runs on to the reference's step count and poisons the colour
+  // with NaN should the ray hit after all (parity tests compare NaN masks)
+  const LinExit mx = miss_exit_init(ro, rd);
+  bool proven_miss = false;
+  // One exit per step (hit | escape | step cap | proven miss), tested with
+  // VALU: a single exec-mask update per iteration.
   for (int i = 1;; ++i) {
 #ifdef RM_STATS
     {
@@ -59,14 +67,21 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       else c.march++;
     }
     hit = d < 0.000001f * t;
-    if (hit | (d > tmax) | (i >= nmax)) break;
-    t += d;
+    bool stop = hit | (d > tmax) | (i >= nmax);
+    t = stop ? t : t + d;
+    if (RM_MISS_EXIT) {
+      const bool gone = !stop && lin_exit(mx, t);
+      if (COUNT) proven_miss |= gone;
+      else stop |= gone;
+    }
+    if (stop) break;
   }
   if (hit) {
     // the opU id (and colour) of the hit: the same sdf at the same point
     const f3 q = add(ro, muls(rd, t));
     scene_exact<true>(q, F.blend, F.omblend, id);
     col = hit_color(id, q);
+    if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
     return t;
   }
   id = -1;
@@ -97,9 +112,9 @@ __device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 #endif
   float res = 1.0f, t = 0.0f;
   int dummy;
-  const ShadowExit ex = shadow_exit_init(F.k, ro, rd);
+  const LinExit ex = shadow_exit_init(F.k, ro, rd);
   for (int i = 0; i < 16; ++i) {
-    if (RM_SHADOW_EXIT && shadow_exit(ex, t)) {  // the remaining steps are no-ops
+    if (RM_SHADOW_EXIT && lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;
       return res;
     }

@@ -392,48 +392,60 @@ __device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id
                        : scene_exact<WANT_ID>(p, blend, omblend, id);
 }
 
-// ---- softshadow early exit ---------------------------------------------------------
-// softshadow (glsl:201-216) always runs 16 steps unless h < 0.001.  Its rd is
-// light - pos, unnormalised (|rd| ~ 10-40), so after 3-4 steps t is past the
-// light and every later step is provably a no-op: with C, R_ALL a sphere
-// enclosing all five bounded primitives and slack(t) = s0 + s1 t the float-error
-// bound of the lazy culler, every float scene value at p(t) = ro + rd t obeys
+// ---- provable early exits (softshadow, misses) ---------------------------------------
+// With C, R_ALL a sphere enclosing all five bounded primitives and
+// slack(t) = s0 + s1 t the float-error bound of the lazy culler, every float
+// scene value at p(t) = ro + rd t obeys
 //   h(t) >= min(|rd| t - |ro - C| - R_ALL,  ro.y + 5.5 + rd.y t) - slack(t).
-// If at t_j both lower bounds, and hence h(t) for all t >= t_j, stay above
-// max(0.001, (1 + 2^-9) t / k), then no later step returns 0.05 and every later
-// k h / t rounds above 1 >= res: the loop's result is `res` now.  With
-// c = (1 + 2^-9) / k (0 for k = inf) the two linear conditions are
-//   a1 t - b1 > 0,  a1 = |rd|lo - s1 - c,         b1 = |ro - C|hi + R_ALL + s0 + 0.001
-//   a2 t + b2 > 0,  a2 = rd.y - s1 - c (> 0),     b2 = ro.y + 5.5 - s0 - 0.001
-// (the second covers the plane's ratio both for b2 + 0.001 >= 0, where a2 > 0 is
+// Both lower bounds are linear in t.  If at t_j both stay above
+// max(hmin, c t) for every t >= t_j, every later step of a march along the ray
+// sees h > hmin and h / t > c:
+//   * softshadow (glsl:201-216; rd = light - pos unnormalised, so t passes the
+//     light after 3-4 steps): hmin = 0.001, c = (1 + 2^-9) / k: no later step
+//     returns 0.05 and every later k h / t rounds above 1 >= res, so the result
+//     is `res` now (16 steps otherwise);
+//   * RayMarch / reflectedRay (glsl:125-161): hmin = 0, c = 1e-6 (1 + 2^-9): no
+//     later step hits (d < 1e-6 t), so the march ends in a miss whatever the
+//     number of steps to d > tmax or the step cap -- and a miss discards t.
+// The two linear conditions are
+//   a1 t - b1 > 0,  a1 = |rd|lo - s1 - c,       b1 = |ro - C|hi + R_ALL + s0 + hmin
+//   a2 t + b2 > 0,  a2 = rd.y - s1 - c (> 0),   b2 = ro.y + 5.5 - s0 - hmin
+// (the second covers the plane's ratio both for b2 + hmin >= 0, where a2 > 0 is
 // enough, and for b2 < 0, where its inf over t >= t_j is at t_j).  Coefficients
-// are rounded toward failure by 2^-12 relative; fma rounding keeps the sign.
+// are rounded toward failure by 2^-12 relative plus 2^-20 absolute; fma rounding
+// keeps the sign.
 constexpr float SH_CX = -5.0f, SH_CY = 0.0f, SH_CZ = -10.0f;
 constexpr float SH_RALL = 23.001f;  // >= max_k |C - c_k| + R_k = 20 + 3 (spheres, torus)
-struct ShadowExit {
+struct LinExit {
   float a1, b1, a2, b2;
 };
-__device__ __forceinline__ ShadowExit shadow_exit_init(float k, f3 ro, f3 rd) {
+__device__ __forceinline__ LinExit lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
   const float LO = 1.0f - 0x1p-12f, HI = 1.0f + 0x1p-12f;
   const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd));
   const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
   const float s0 = 0x1p-14f * (ro1 * HI + 64.0f) * HI;
   const float s1 = 0x1p-14f * rdl * (HI * HI);
-  const float c = (k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / k * HI;
   const float ex = ro.x - SH_CX, ey = ro.y - SH_CY, ez = ro.z - SH_CZ;
   const float rc = __builtin_fmaf(__builtin_amdgcn_sqrtf((ex * ex + ey * ey) + ez * ez), HI, 0x1p-18f);
-  ShadowExit e;
+  LinExit e;
   // absolute 2^-20 terms: the rounding of a difference is relative to its
   // operands, not to a small (cancelled) result
   e.a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
-  e.b1 = (rc + SH_RALL + s0 + 0.001f) * HI;
+  e.b1 = (rc + SH_RALL + s0 + hmin) * HI;
   e.a2 = (rd.y - s1 - c) * LO - 0x1p-20f * (fabsf(rd.y) + s1 + c);
-  e.b2 = ((ro.y + 5.5f) - s0 - 0.001f * HI) - 0x1p-19f * (fabsf(ro.y) + 6.5f + s0);
+  e.b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
   if (!(e.a1 > 0.0f)) e.b1 = __builtin_huge_valf();   // never exits
   if (!(e.a2 > 0.0f)) e.b2 = -__builtin_huge_valf();
   return e;
 }
-__device__ __forceinline__ bool shadow_exit(const ShadowExit& e, float t) {
+__device__ __forceinline__ LinExit shadow_exit_init(float k, f3 ro, f3 rd) {
+  const float c = (k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / k * (1.0f + 0x1p-12f);
+  return lin_exit_init(c, 0.001f, ro, rd);
+}
+__device__ __forceinline__ LinExit miss_exit_init(f3 ro, f3 rd) {
+  return lin_exit_init(0.000001f * (1.0f + 0x1p-9f), 0.0f, ro, rd);
+}
+__device__ __forceinline__ bool lin_exit(const LinExit& e, float t) {
   return (__builtin_fmaf(e.a1, t, -e.b1) > 0.0f) & (__builtin_fmaf(e.a2, t, e.b2) > 0.0f);
 }
 

@@ -35,6 +35,9 @@
 #ifndef RM_SHADOW_EXIT
 #define RM_SHADOW_EXIT 1
 #endif
+#ifndef RM_MISS_EXIT
+#define RM_MISS_EXIT 1
+#endif
 
 namespace rmd {
 
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
   int hid = -1;                        // id of the current hit (-1 = miss)
   float hchk = 0.f;                    // checkers() at the current hit point
   float res = 1.f;                     // softshadow running minimum
-  ShadowExit sx = {0.f, 0.f, 0.f, 0.f};  // softshadow early-exit bounds (rm_scene.hpp)
+  LinExit sx = {0.f, 0.f, 0.f, 0.f};  // early-exit bounds of the current march / shadow
   uint32_t c_pix = 0;
   uint32_t c_rays = 0, c_march = 0, c_refl = 0, c_shadow = 0, c_norm = 0, c_light = 0;
   uint32_t c_iters = 0;
@@ -101,6 +104,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
     t = 0.f;
     i = 0;
     bi = 0;
+    sx = miss_exit_init(ro, rd);
     phase = PH_MARCH;
     if (COUNT) c_rays++;
   };
@@ -143,6 +147,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
               ro = add(pos, muls(nrm, 0.001f));
               t = 0.f;
               i = 0;
+              sx = miss_exit_init(ro, rd);
               phase = PH_MARCH;
             } else {
               add_sample(col);
@@ -182,6 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
               ro = add(pos, muls(nrm, 0.001f));
               t = 0.f;
               i = 0;
+              sx = miss_exit_init(ro, rd);
               phase = PH_MARCH;
             }
           }
@@ -278,6 +284,8 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
           t += d;
           ++i;
           miss = (i >= (bi == 0 ? 512 : 256));
+          // provable miss (rm_scene.hpp "early exits"); counting runs the full march
+          if (!COUNT && RM_MISS_EXIT && lin_exit(sx, t)) miss = true;
         }
       }
       if (hit) {
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
         t += d;
         ++i;
         done = (i >= 16);
-        if (!done && RM_SHADOW_EXIT && shadow_exit(sx, t)) {  // the remaining steps are no-ops
+        if (!done && RM_SHADOW_EXIT && lin_exit(sx, t)) {  // the remaining steps are no-ops
           if (COUNT) {
             c_shadow += 16 - i;
             c_pix += 16 - i;

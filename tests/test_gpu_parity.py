@@ -71,6 +71,15 @@ def test_parity_vs_oracle(rm, oracle, gpu, case, kernel):
     k = rm.RM_KERNEL_PIXEL if kernel == "pixel" else rm.RM_KERNEL_WAVEQUEUE
     got = _render_gpu(rm, u, W, H, k)
     _compare(ref, got, f"{kernel} {case}")
+    _production_equals_counting(rm, u, W, H, k, got, f"{kernel} {case}")
+
+
+def _production_equals_counting(rm, u, W, H, k, counted, label):
+    """The production build (no counters) takes the proof-based early exits
+    that the counting build only checks; both must give the same image."""
+    prod = _render_gpu(rm, u, W, H, k, counters=False)
+    np.testing.assert_array_equal(prod["rgba32f"], counted["rgba32f"], err_msg=label)
+    np.testing.assert_array_equal(prod["rgba8"], counted["rgba8"], err_msg=label)
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (3, 1), (1, 5), (37, 23), (65, 3), (130, 67)])
@@ -146,3 +155,4 @@ def test_stress_uniforms(rm, oracle, gpu, case, bounces, aa, sm):
     for k in (rm.RM_KERNEL_PIXEL, rm.RM_KERNEL_WAVEQUEUE):
         got = _render_gpu(rm, u, W, H, k)
         _compare(ref, got, f"{name} kernel {k}")
+        _production_equals_counting(rm, u, W, H, k, got, f"{name} kernel {k}")
