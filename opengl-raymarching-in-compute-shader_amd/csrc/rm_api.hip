@@ -237,11 +237,15 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   c->own_stream = true;
   if (c->cfg.outputs & RM_OUT_RGBA8) {
     if ((e = hipMalloc(&c->d_rgba8, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc rgba8"));
-    if ((e = hipMemset(c->d_rgba8, 0, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
+    // on the context's own (non-blocking) stream: a NULL-stream memset is not
+    // ordered before kernels on it and could land after the first dispatch
+    if ((e = hipMemsetAsync(c->d_rgba8, 0, npx * 4, c->stream)) != hipSuccess)
+      return bail(hip_fail(c, e, "hipMemset"));
   }
   if (c->cfg.outputs & RM_OUT_RGBA32F) {
     if ((e = hipMalloc(&c->d_rgba32f, npx * 16)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc rgba32f"));
-    if ((e = hipMemset(c->d_rgba32f, 0, npx * 16)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
+    if ((e = hipMemsetAsync(c->d_rgba32f, 0, npx * 16, c->stream)) != hipSuccess)
+      return bail(hip_fail(c, e, "hipMemset"));
   }
   if (c->cfg.counters) {
     if ((e = hipMalloc(&c->d_counts, npx * 4)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc counts"));
@@ -249,6 +253,7 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
       return bail(hip_fail(c, e, "hipMalloc counters"));
   }
   if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipStreamSynchronize"));
   rm_default_uniforms(&c->u);
   // Tuning knobs of the wave-queue kernel; defaults are the tuned values.
   if (const char* e = std::getenv("RM_WQ_BATCH")) rm::g_wq_batch = std::atoi(e);

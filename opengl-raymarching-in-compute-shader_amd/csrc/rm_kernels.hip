@@ -23,14 +23,39 @@
 
 namespace rmd {
 
+#ifdef RM_PHASE_TIMING
+// Diagnostic build only: wave clock cycles spent per phase (tools/phase_probe.hip).
+// RM_PT(k, v) charges the time since the previous mark to phase k once v (the
+// phase's result) is computed; volatile asm keeps the marks in program order.
+__device__ unsigned long long g_phase[16];
+__device__ __forceinline__ unsigned long long pt_clock() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+#define RM_PT_BEGIN() unsigned long long pt_t0_ = pt_clock()
+#define RM_PT(k, v)                                                            \
+  do {                                                                         \
+    asm volatile("" ::"v"(v));                                                 \
+    const unsigned long long now_ = pt_clock();                                \
+    const unsigned long long m_ = __ballot(1);                                 \
+    if (__lane_id() == __builtin_ffsll(m_) - 1) atomicAdd(&g_phase[k], now_ - pt_t0_); \
+    pt_t0_ = pt_clock();                                                       \
+  } while (0)
+#else
+#define RM_PT_BEGIN() do {} while (0)
+#define RM_PT(k, v) do {} while (0)
+#endif
+
 struct Cnt {
   uint32_t rays, march, reflect, shadow, normals, lights;
 };
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161.  Returns t or -1.
 template <bool COUNT>
-__device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c) {
-  float t = 0.0f;
+__device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
+                       float& dlast) {
+  float t = 0.0f, dl = 0.0f;
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   bool hit = false;
@@ -67,6 +92,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       else c.march++;
     }
     hit = d < 0.000001f * t;
+    dl = d;
     bool stop = hit | (d > tmax) | (i >= nmax);
     t = stop ? t : t + d;
     if (RM_MISS_EXIT) {
@@ -82,6 +108,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     scene_exact<true>(q, F.blend, F.omblend, id);
     col = hit_color(id, q);
     if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
+    dlast = dl;
     return t;
   }
   id = -1;
@@ -90,18 +117,25 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 }
 
 // GetNormal glsl:278-288
-template <bool COUNT>
-__device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c) {
+// GetNormal glsl:278-288, samples with shared culling (rm_scene.hpp).  HAVE_C0:
+// the centre sample sdf(pos) is the primary march's last distance (same point).
+#ifndef RM_NORMAL_INLINE
+#define RM_NORMAL_INLINE 0
+#endif
+template <bool COUNT, bool HAVE_C0>
+#if RM_NORMAL_INLINE
+__device__ __forceinline__
+#else
+__device__
+#endif
+f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
 #ifdef RM_ABL_NO_NORMAL
   return mk(0.0f, 1.0f, 0.0f);
 #endif
-  int dummy;
   if (COUNT) c.normals++;
-  float cc = scene<false>(pos, F.blend, F.omblend, dummy);
-  f3 v = mk(scene<false>(add(pos, mk(0.001f, 0.0f, 0.0f)), F.blend, F.omblend, dummy),
-            scene<false>(add(pos, mk(0.0f, 0.001f, 0.0f)), F.blend, F.omblend, dummy),
-            scene<false>(add(pos, mk(0.0f, 0.0f, 0.001f)), F.blend, F.omblend, dummy));
-  return normalize(subs(v, cc));
+  float vx, vy, vz;
+  normal_samples<HAVE_C0>(pos, F.blend, F.omblend, c0, vx, vy, vz);
+  return normalize(subs(mk(vx, vy, vz), c0));
 }
 
 // softshadow glsl:201-216
@@ -139,23 +173,30 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     // After a MATTE prevObject every remaining iteration is a colour no-op
     // (glsl:181,189-190): stop instead of running the dead marches.
     if (prevMatte) break;
+    RM_PT_BEGIN();
     rayDir = reflect(rayDir, normal);
     int id;
     f3 tcol;
-    float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c);
+    float dl;
+    float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c, dl);
+    RM_PT(4, th);
     pos = add(pos, muls(rayDir, th));
     // The normal of a miss on the last bounce is never read: skip it.
-    if (th != -1.0f || i < F.bounces) normal = get_normal<COUNT>(F, pos, c);
+    // (the hit point is pos + rayDir t, not the march's ro + rd t: no centre reuse)
+    if (th != -1.0f || i < F.bounces) normal = get_normal<COUNT, false>(F, pos, c);
+    RM_PT(5, normal.x);
     if (th == -1.0f) {
       tcol = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
     } else {
       if (COUNT) c.lights++;
       tcol = point_light(F, tcol, normal, pos);
     }
+    RM_PT(6, tcol.x);
     if (id == 7 && !prevMatte && i < 3) {
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
       color = muls(color, sh / (float)i);
     }
+    RM_PT(7, color.x);
     color = add(color, divs(mul(tcol, prevColor), (float)i));
     prevColor = tcol;
     prevMatte = (id == 7);  // material of the hit: MATTE only for the floor; dummy is 1.0
@@ -169,16 +210,22 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   int id;
   f3 hcol;
-  float th = march<COUNT>(F, ro, rd, false, id, hcol, c);
+  RM_PT_BEGIN();
+  float dl;
+  float th = march<COUNT>(F, ro, rd, false, id, hcol, c, dl);
+  RM_PT(0, th);
   if (th != -1.0f) {
     f3 pos = add(ro, muls(rd, th));
-    f3 normal = get_normal<COUNT>(F, pos, c);
+    f3 normal = get_normal<COUNT, true>(F, pos, c, dl);
+    RM_PT(1, normal.x);
     if (COUNT) c.lights++;
     color = point_light(F, hcol, normal, pos);
+    RM_PT(2, color.x);
     if (id == 7) {
       f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
       color = muls(color, sh);
+      RM_PT(3, color.x);
       return gamma(color);
     }
     if (F.bounces > 0) color = bounce<COUNT>(F, rd, pos, normal, color, hcol, c);
@@ -269,6 +316,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   const int py = global_row(F, lrow);
   Cnt c = {0, 0, 0, 0, 0, 0};
   f3 col = mk(0.0f, 0.0f, 0.0f);
+  RM_PT_BEGIN();
   if (py >= 0) {
     float x = (float)(px * 2 - F.width) / (float)F.width;
     float y = (float)(py * 2 - F.height) / (float)F.height;
@@ -297,6 +345,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
     atomicAdd(&F.counters[4], (unsigned long long)c.normals);
     atomicAdd(&F.counters[5], (unsigned long long)c.lights);
   }
+  RM_PT(8, col.x);
   if (s != 0) return;
   if (py >= 0) {
     const float o0 = ((col.x + r1) + r2) + r3, o1 = ((col.y + g1) + g2) + g3,

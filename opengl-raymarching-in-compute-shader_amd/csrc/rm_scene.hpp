@@ -260,6 +260,86 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   return m;
 }
 
+// ---- GetNormal's samples with shared culling (glsl:278-288) --------------------------
+// sdf at pos and at pos + 0.001 e_x/e_y/e_z.  The four points lie within
+// e = 0.001 + 2^-22 (|pos|_1 + 1) of pos (the float adds round), so by the
+// 1-Lipschitz property one set of bounds at pos culls primitive k at all four:
+//   LB_k(p') >= LB_k(pos) - e,   U(p') <= U(pos) + e   =>   cull if LB_k(pos) - 2e > U(pos).
+// The survivors are evaluated exactly at each point (the same float ops as
+// scene_exact), so every value is the exact float minimum.  With HAVE_C0 the
+// centre value is the march's last distance at this very point (render's
+// pos == the march's final q, glsl:226 vs :129): only three points remain.
+__device__ __forceinline__ float ev_sph0(f3 p) {
+  const Offs o = offsets(p);
+  return sqrt_core((o.ax * o.ax + o.ay2) + o.az2) - 3.0f;
+}
+__device__ __forceinline__ float ev_sph1(f3 p) {
+  const Offs o = offsets(p);
+  return sqrt_core((o.bx * o.bx + o.ay2) + o.az2) - 3.0f;
+}
+__device__ __forceinline__ float ev_blend(f3 p, float blend, float omblend) {
+  const Offs o = offsets(p);
+  return sd_blend(o, (o.cx2 + o.ay2) + o.az2, blend, omblend);
+}
+__device__ __forceinline__ float ev_torus(f3 p) { return sd_torus(offsets(p), p.z - 10.0f); }
+__device__ __forceinline__ float ev_capsule(f3 p) { return sd_capsule(offsets(p), p); }
+
+template <bool HAVE_C0>
+__device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblend, float& c0,
+                                               float& vx, float& vy, float& vz) {
+  const f3 px = add(pos, mk(0.001f, 0.0f, 0.0f));
+  const f3 py = add(pos, mk(0.0f, 0.001f, 0.0f));
+  const f3 pz = add(pos, mk(0.0f, 0.0f, 0.001f));
+  const Offs o = offsets(pos);
+  const float tz = pos.z - 10.0f;
+  const float kx = pos.x - CAP_MX, ky = pos.y - CAP_MY, kz = pos.z - CAP_MZ;
+  const float r0 = __builtin_amdgcn_sqrtf((o.ax * o.ax + o.ay2) + o.az2);
+  const float r1 = __builtin_amdgcn_sqrtf((o.bx * o.bx + o.ay2) + o.az2);
+  const float rs = __builtin_amdgcn_sqrtf((o.cx2 + o.ay2) + o.az2);
+  const float rt = __builtin_amdgcn_sqrtf((o.cx2 + o.ay2) + tz * tz);
+  const float rk = __builtin_amdgcn_sqrtf((kx * kx + ky * ky) + kz * kz);
+  const float e2 = 2.0f * (0.001f + 0x1p-22f * (((fabsf(pos.x) + fabsf(pos.y)) + fabsf(pos.z)) + 1.0f));
+  float U = vmin(pos.y + 5.5f, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
+  U = vmin3(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f),
+            __builtin_fmaf(rs, CULL_REL_HI, CULL_ABS - 2.5f));
+  U = U + e2;  // U(pos) + e, compared with LB(pos) - e; 2e absorbs the add's rounding
+  float mc = pos.y + 5.5f, mx = px.y + 5.5f, my = py.y + 5.5f, mz = pz.y + 5.5f;
+  if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    if (!HAVE_C0) mc = vmin(mc, ev_sph0(pos));
+    mx = vmin(mx, ev_sph0(px));
+    my = vmin(my, ev_sph0(py));
+    mz = vmin(mz, ev_sph0(pz));
+  }
+  if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
+    if (!HAVE_C0) mc = vmin(mc, ev_sph1(pos));
+    mx = vmin(mx, ev_sph1(px));
+    my = vmin(my, ev_sph1(py));
+    mz = vmin(mz, ev_sph1(pz));
+  }
+  if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {
+    if (!HAVE_C0) mc = vmin(mc, ev_blend(pos, blend, omblend));
+    mx = vmin(mx, ev_blend(px, blend, omblend));
+    my = vmin(my, ev_blend(py, blend, omblend));
+    mz = vmin(mz, ev_blend(pz, blend, omblend));
+  }
+  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {
+    if (!HAVE_C0) mc = vmin(mc, ev_torus(pos));
+    mx = vmin(mx, ev_torus(px));
+    my = vmin(my, ev_torus(py));
+    mz = vmin(mz, ev_torus(pz));
+  }
+  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {
+    if (!HAVE_C0) mc = vmin(mc, ev_capsule(pos));
+    mx = vmin(mx, ev_capsule(px));
+    my = vmin(my, ev_capsule(py));
+    mz = vmin(mz, ev_capsule(pz));
+  }
+  if (!HAVE_C0) c0 = mc;
+  vx = mx;
+  vy = my;
+  vz = mz;
+}
+
 // ---- lazy culling along a ray ------------------------------------------------------
 // For a march p(t) = ro + rd*t.  Primitive k is skipped while t < te[k].  When k
 // is re-tested at p_i (t_i) with U_i >= min(p_i) and LB_k(p_i) > U_i, then for
