@@ -56,6 +56,7 @@ template <bool COUNT>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
                        float& dlast) {
   float t = 0.0f, dl = 0.0f;
+  int idl = 7;  // opU id of the last step's minimum
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   bool hit = false;
@@ -66,7 +67,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // provable miss (rm_scene.hpp "early exits"): production stops there; the
   // counting build runs on to the reference's step count and poisons the colour
   // with NaN should the ray hit after all (parity tests compare NaN masks)
-  const LinExit mx = miss_exit_init(ro, rd);
+  const float mx = miss_exit_init(ro, rd);
   bool proven_miss = false;
   // One exit per step (hit | escape | step cap | proven miss), tested with
   // VALU: a single exec-mask update per iteration.
@@ -82,10 +83,9 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #endif
     const f3 q = add(ro, muls(rd, t));
 #if RM_LAZY_CULL
-    const float d = scene_lazy(q, t, lc, F.blend, F.omblend);
+    const float d = scene_lazy(q, t, lc, F.blend, F.omblend, idl);
 #else
-    int dummy;
-    const float d = scene<false>(q, F.blend, F.omblend, dummy);
+    const float d = scene<true>(q, F.blend, F.omblend, idl);
 #endif
     if (COUNT) {
       if (reflected) c.reflect++;
@@ -103,9 +103,9 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     if (stop) break;
   }
   if (hit) {
-    // the opU id (and colour) of the hit: the same sdf at the same point
+    // the opU id (and colour) of the hit: from the last step's sdf (same point)
     const f3 q = add(ro, muls(rd, t));
-    scene_exact<true>(q, F.blend, F.omblend, id);
+    id = idl;
     col = hit_color(id, q);
     if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
     dlast = dl;
@@ -146,7 +146,7 @@ __device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 #endif
   float res = 1.0f, t = 0.0f;
   int dummy;
-  const LinExit ex = shadow_exit_init(F.k, ro, rd);
+  const float ex = shadow_exit_init(F.k, ro, rd);
   for (int i = 0; i < 16; ++i) {
     if (RM_SHADOW_EXIT && lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;

@@ -401,11 +401,24 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
 #define RM_LZ_BLOCK(c) (c)
 #endif
 
+// id: the opU id of the minimum (glsl:105,110-121), as scene_exact<true> gives
+// it: the primitives are taken in the reference's order with ties going to the
+// later one, the plane last; culled primitives are strictly above the minimum
+// and can neither win nor tie.
 __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend,
-                                            float omblend) {
+                                            float omblend, int& id) {
   float m = p.y + 5.5f;  // plane, exact (glsl:85,121); running minimum
+  id = 7;
   RM_STAT(8);
   if (RM_LZ_BLOCK(t >= lc.temin)) {
+    const float plane = m;
+    float mp = __builtin_huge_valf();  // minimum over the evaluated primitives
+    int idp = 7;
+    auto take = [&](float v, int k) {
+      idp = (v <= mp) ? k : idp;
+      mp = vmin(mp, v);
+      m = vmin(m, v);
+    };
     RM_STAT(9);
     const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
     const float inv2v = lc.inv2v, invp = lc.invp;
@@ -426,38 +439,39 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
       if (retest(x0, 3.0f, lc.te[0])) {
         RM_STAT(10);
-        m = vmin(m, sqrt_core(x0) - 3.0f);
+        take(sqrt_core(x0) - 3.0f, 0);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
       if (retest(x1, 3.0f, lc.te[1])) {
         RM_STAT(11);
-        m = vmin(m, sqrt_core(x1) - 3.0f);
+        take(sqrt_core(x1) - 3.0f, 1);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
       if (retest(xs, R_BLEND_LO, lc.te[2])) {
         RM_STAT(12);
-        m = vmin(m, sd_blend(o, xs, blend, omblend));
+        take(sd_blend(o, xs, blend, omblend), 4);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
       if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3])) {
         RM_STAT(13);
-        m = vmin(m, sd_torus(o, tz));
+        take(sd_torus(o, tz), 5);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
       if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
         RM_STAT(14);
-        m = vmin(m, sd_capsule(o, p));
+        take(sd_capsule(o, p), 6);
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
+    id = (plane <= mp) ? 7 : idp;
   }
   return m;
 }
@@ -492,14 +506,13 @@ __device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id
 //   a2 t + b2 > 0,  a2 = rd.y - s1 - c (> 0),   b2 = ro.y + 5.5 - s0 - hmin
 // (the second covers the plane's ratio both for b2 + hmin >= 0, where a2 > 0 is
 // enough, and for b2 < 0, where its inf over t >= t_j is at t_j).  Coefficients
-// are rounded toward failure by 2^-12 relative plus 2^-20 absolute; fma rounding
-// keeps the sign.
+// are rounded toward failure by 2^-12 relative plus 2^-20 absolute.  Both hold
+// for t > T = max(b1 / a1, -b2 / a2) (+inf unless a1, a2 > 0); T is rounded up
+// (v_rcp_f32 is within 1 ulp; the 2^-20 factor covers it and the two products),
+// so the per-step test is one compare, t > T.
 constexpr float SH_CX = -5.0f, SH_CY = 0.0f, SH_CZ = -10.0f;
 constexpr float SH_RALL = 23.001f;  // >= max_k |C - c_k| + R_k = 20 + 3 (spheres, torus)
-struct LinExit {
-  float a1, b1, a2, b2;
-};
-__device__ __forceinline__ LinExit lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
+__device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
   const float LO = 1.0f - 0x1p-12f, HI = 1.0f + 0x1p-12f;
   const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd));
   const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
@@ -507,27 +520,26 @@ __device__ __forceinline__ LinExit lin_exit_init(float c, float hmin, f3 ro, f3 
   const float s1 = 0x1p-14f * rdl * (HI * HI);
   const float ex = ro.x - SH_CX, ey = ro.y - SH_CY, ez = ro.z - SH_CZ;
   const float rc = __builtin_fmaf(__builtin_amdgcn_sqrtf((ex * ex + ey * ey) + ez * ez), HI, 0x1p-18f);
-  LinExit e;
   // absolute 2^-20 terms: the rounding of a difference is relative to its
   // operands, not to a small (cancelled) result
-  e.a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
-  e.b1 = (rc + SH_RALL + s0 + hmin) * HI;
-  e.a2 = (rd.y - s1 - c) * LO - 0x1p-20f * (fabsf(rd.y) + s1 + c);
-  e.b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
-  if (!(e.a1 > 0.0f)) e.b1 = __builtin_huge_valf();   // never exits
-  if (!(e.a2 > 0.0f)) e.b2 = -__builtin_huge_valf();
-  return e;
+  const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
+  const float b1 = (rc + SH_RALL + s0 + hmin) * HI;
+  const float a2 = (rd.y - s1 - c) * LO - 0x1p-20f * (fabsf(rd.y) + s1 + c);
+  const float b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
+  const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
+  const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * UP;
+  const float T2 = -(b2 * __builtin_amdgcn_rcpf(a2) * (b2 >= 0.0f ? DN : UP));
+  const float INF = __builtin_huge_valf();
+  return (a1 > 0.0f && a2 > 0.0f) ? __builtin_fmaxf(T1, T2) : INF;
 }
-__device__ __forceinline__ LinExit shadow_exit_init(float k, f3 ro, f3 rd) {
+__device__ __forceinline__ float shadow_exit_init(float k, f3 ro, f3 rd) {
   const float c = (k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / k * (1.0f + 0x1p-12f);
   return lin_exit_init(c, 0.001f, ro, rd);
 }
-__device__ __forceinline__ LinExit miss_exit_init(f3 ro, f3 rd) {
+__device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) {
   return lin_exit_init(0.000001f * (1.0f + 0x1p-9f), 0.0f, ro, rd);
 }
-__device__ __forceinline__ bool lin_exit(const LinExit& e, float t) {
-  return (__builtin_fmaf(e.a1, t, -e.b1) > 0.0f) & (__builtin_fmaf(e.a2, t, e.b2) > 0.0f);
-}
+__device__ __forceinline__ bool lin_exit(float T, float t) { return t > T; }
 
 // softshadow's  res = min(res, k * h / t)  (glsl:211), exactly.  The quotient
 // only matters when it is below res, so it is first bounded with v_rcp_f32

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
   int hid = -1;                        // id of the current hit (-1 = miss)
   float hchk = 0.f;                    // checkers() at the current hit point
   float res = 1.f;                     // softshadow running minimum
-  LinExit sx = {0.f, 0.f, 0.f, 0.f};  // early-exit bounds of the current march / shadow
+  float sx = 0.f;                          // early-exit bounds of the current march / shadow
   uint32_t c_pix = 0;
   uint32_t c_rays = 0, c_march = 0, c_refl = 0, c_shadow = 0, c_norm = 0, c_light = 0;
   uint32_t c_iters = 0;
