@@ -112,6 +112,13 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.omblend = 1.0f - F.blend;
   F.k = (u.shadow_mode == RM_SHADOW_HARD) ? INFINITY : 2.0f;
   F.persp = 45.0f * static_cast<float>(0.01745329251994329576923690768489);
+  {
+    const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f}, oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
+    for (int k = 0; k < 4; ++k) {
+      F.aa_dx[k] = ox[k] / (float)c->cfg.width;
+      F.aa_dy[k] = oy[k] / (float)c->cfg.height;
+    }
+  }
   F.bounces = u.bounceVar;
   F.aa = u.AA ? 1 : 0;
   F.width = c->cfg.width;

@@ -51,6 +51,15 @@ struct Cnt {
   uint32_t rays, march, reflect, shadow, normals, lights;
 };
 
+// Cost probes (diagnostic builds only, tools/build_variant.sh): RM_DBL_<PHASE>
+// runs a phase twice on an opaque copy of its inputs and folds the copy in as
+// a no-op, so the time difference is that phase's marginal cost.
+__device__ __forceinline__ float opaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ f3 opaque(f3 v) { return mk(opaque(v.x), opaque(v.y), opaque(v.z)); }
+
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161.  Returns t or -1.
 template <bool COUNT>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
@@ -135,12 +144,28 @@ f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
   if (COUNT) c.normals++;
   float vx, vy, vz;
   normal_samples<HAVE_C0>(pos, F.blend, F.omblend, c0, vx, vy, vz);
+#ifdef RM_DBL_NORMAL
+  if (!COUNT) {
+    float c0b = c0, wx, wy, wz;
+    normal_samples<HAVE_C0>(opaque(pos), F.blend, F.omblend, c0b, wx, wy, wz);
+    vx = vmin(vx, wx); vy = vmin(vy, wy); vz = vmin(vz, wz); c0 = vmin(c0, c0b);
+  }
+#endif
   return normalize(subs(mk(vx, vy, vz), c0));
 }
 
 // softshadow glsl:201-216
 template <bool COUNT>
-__device__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+__device__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c);
+template <bool COUNT>
+__device__ __forceinline__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+#ifdef RM_DBL_SHADOW
+  if (!COUNT) return vmin(softshadow_impl<COUNT>(F, ro, rd, c), softshadow_impl<COUNT>(F, opaque(ro), rd, c));
+#endif
+  return softshadow_impl<COUNT>(F, ro, rd, c);
+}
+template <bool COUNT>
+__device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 #ifdef RM_ABL_NO_SHADOW
   return 1.0f;
 #endif
@@ -179,6 +204,13 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     f3 tcol;
     float dl;
     float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c, dl);
+#ifdef RM_DBL_BMARCH
+    if (!COUNT) {
+      int id2; f3 tc2; float dl2;
+      const float th2 = march<COUNT>(F, opaque(add(pos, muls(normal, 0.001f))), rayDir, true, id2, tc2, c, dl2);
+      th = (th2 == th) ? th : __builtin_nanf("");
+    }
+#endif
     RM_PT(4, th);
     pos = add(pos, muls(rayDir, th));
     // The normal of a miss on the last bounce is never read: skip it.
@@ -213,6 +245,13 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   RM_PT_BEGIN();
   float dl;
   float th = march<COUNT>(F, ro, rd, false, id, hcol, c, dl);
+#ifdef RM_DBL_MARCH
+  if (!COUNT) {
+    int id2; f3 hc2; float dl2;
+    const float th2 = march<COUNT>(F, opaque(ro), rd, false, id2, hc2, c, dl2);
+    th = (th2 == th) ? th : __builtin_nanf("");
+  }
+#endif
   RM_PT(0, th);
   if (th != -1.0f) {
     f3 pos = add(ro, muls(rd, th));
@@ -220,6 +259,12 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     RM_PT(1, normal.x);
     if (COUNT) c.lights++;
     color = point_light(F, hcol, normal, pos);
+#ifdef RM_DBL_LIGHT
+    if (!COUNT) {
+      const f3 c2 = point_light(F, hcol, normal, opaque(pos));
+      color = mk(vmin(color.x, c2.x), vmin(color.y, c2.y), vmin(color.z, c2.z));
+    }
+#endif
     RM_PT(2, color.x);
     if (id == 7) {
       f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
@@ -230,6 +275,12 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     }
     if (F.bounces > 0) color = bounce<COUNT>(F, rd, pos, normal, color, hcol, c);
   }
+#ifdef RM_DBL_GAMMA
+  if (!COUNT) {
+    const f3 g1 = gamma(color), g2 = gamma(opaque(color));
+    return mk(vmin(g1.x, g2.x), vmin(g1.y, g2.y), vmin(g1.z, g2.z));
+  }
+#endif
   return gamma(color);
 }
 
@@ -258,12 +309,10 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
     float y = (float)(py * 2 - F.height) / (float)F.height;
     f3 ro, rd;
     if (F.aa) {
-      const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f};
-      const float oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
 #pragma unroll 1
       for (int s = 0; s < 4; ++s) {
-        x += ox[s] / (float)F.width;
-        y += oy[s] / (float)F.height;
+        x += F.aa_dx[s];
+        y += F.aa_dy[s];
         cast_ray(F, x, y, ro, rd);
         if (COUNT) c.rays++;
         f3 col = render<COUNT>(F, ro, rd, c);
@@ -320,11 +369,9 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   if (py >= 0) {
     float x = (float)(px * 2 - F.width) / (float)F.width;
     float y = (float)(py * 2 - F.height) / (float)F.height;
-    const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f};
-    const float oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
     for (int j = 0; j <= s; ++j) {
-      x += ox[j] / (float)F.width;
-      y += oy[j] / (float)F.height;
+      x += F.aa_dx[j];
+      y += F.aa_dy[j];
     }
     f3 ro, rd;
     cast_ray(F, x, y, ro, rd);

@@ -32,8 +32,10 @@ __device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, 
 __device__ __forceinline__ f3 subs(f3 a, float s) { return mk(a.x - s, a.y - s, a.z - s); }
 __device__ __forceinline__ f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ float len(f3 a) { return __builtin_sqrtf(dot(a, a)); }
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / __builtin_sqrtf(dot(a, a))); }
+// sqrt_cr_nonneg == the correctly rounded sqrt on [0, FLT_MAX] (rm_fastmath.hpp),
+// with NaN and +inf passing through unchanged
+__device__ __forceinline__ float len(f3 a) { return sqrt_cr_nonneg(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / sqrt_cr_nonneg(dot(a, a))); }
 // v_min_f32 / v_min3_f32 without the NaN-quieting canonicalisations LLVM adds
 // when it cannot prove an operand canonical (values merged from branches).
 // All operands here are finite sdf values or +inf, never NaN.
@@ -61,6 +63,7 @@ struct Frame {
   float omblend;   // 1 - blend (uniform-only subexpression of mix)
   float k;         // softshadow k: 2.0 (glsl:185,236) or +inf (hard-shadow extension)
   float persp;     // radians(45) = 45 * 0.017453292519943295f (glsl:70)
+  float aa_dx[4], aa_dy[4];  // offsetX[s] / dims.x, offsetY[s] / dims.y (glsl:311-332), host IEEE
   int32_t bounces; // bounceVar, 0..5
   int32_t aa;      // AA
   int32_t width, height;
@@ -390,6 +393,9 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
 #ifndef RM_LAZY_ALL
 #define RM_LAZY_ALL 0
 #endif
+#ifndef RM_LAZY_EXACT_TE
+#define RM_LAZY_EXACT_TE 0
+#endif
 #if RM_LAZY_ALL
 #define RM_LZ_ANY(c) true
 #define RM_LZ_BLOCK(c) __any(c)
@@ -414,15 +420,22 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
     const float plane = m;
     float mp = __builtin_huge_valf();  // minimum over the evaluated primitives
     int idp = 7;
-    auto take = [&](float v, int k) {
-      idp = (v <= mp) ? k : idp;
-      mp = vmin(mp, v);
-      m = vmin(m, v);
-    };
+
     RM_STAT(9);
     const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
     const float inv2v = lc.inv2v, invp = lc.invp;
     const float pl = m + slack;  // plane(p_i) + slack
+    // an exactly evaluated k: its value bounds it like LB does (RM_LAZY_EXACT_TE),
+    // so a k that is not the minimum gets a budget instead of a re-test next step
+    auto take = [&](float v, int k, float& te) {
+      if (RM_LAZY_EXACT_TE) {
+        const float g = v - m - slack;
+        if (g > 0.0f) te = t + __builtin_fmaxf(g * inv2v, (v - pl) * invp);
+      }
+      idp = (v <= mp) ? k : idp;
+      mp = vmin(mp, v);
+      m = vmin(m, v);
+    };
     // re-test k; returns true when k must be evaluated exactly at this step
     auto retest = [&](float x, float R, float& te) -> bool {
       RM_STAT(1);
@@ -439,35 +452,35 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
       if (retest(x0, 3.0f, lc.te[0])) {
         RM_STAT(10);
-        take(sqrt_core(x0) - 3.0f, 0);
+        take(sqrt_core(x0) - 3.0f, 0, lc.te[0]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
       if (retest(x1, 3.0f, lc.te[1])) {
         RM_STAT(11);
-        take(sqrt_core(x1) - 3.0f, 1);
+        take(sqrt_core(x1) - 3.0f, 1, lc.te[1]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
       if (retest(xs, R_BLEND_LO, lc.te[2])) {
         RM_STAT(12);
-        take(sd_blend(o, xs, blend, omblend), 4);
+        take(sd_blend(o, xs, blend, omblend), 4, lc.te[2]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
       if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3])) {
         RM_STAT(13);
-        take(sd_torus(o, tz), 5);
+        take(sd_torus(o, tz), 5, lc.te[3]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
       if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
         RM_STAT(14);
-        take(sd_capsule(o, p), 6);
+        take(sd_capsule(o, p), 6, lc.te[4]);
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
@@ -625,7 +638,7 @@ __device__ __forceinline__ void cast_ray(const Frame& F, float uvx, float uvy, f
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = (uvx * F.cam_x[k] + uvy * F.cam_y[k]) + F.cam_dir[k] * F.persp;
   float dd = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-  float inv = 1.0f / __builtin_sqrtf(dd);
+  float inv = 1.0f / sqrt_cr_nonneg(dd);
   ro = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
   rd = mk(v[0] * inv, v[1] * inv, v[2] * inv);
 }
