@@ -65,7 +65,9 @@ template <bool COUNT>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
                        float& dlast) {
   float t = 0.0f, dl = 0.0f;
+#if !RM_LAZY_CULL
   int idl = 7;  // opU id of the last step's minimum
+#endif
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   bool hit = false;
@@ -90,11 +92,10 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       }
     }
 #endif
-    const f3 q = add(ro, muls(rd, t));
 #if RM_LAZY_CULL
-    const float d = scene_lazy(q, t, lc, F.blend, F.omblend, idl);
+    const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
 #else
-    const float d = scene<true>(q, F.blend, F.omblend, idl);
+    const float d = scene<true>(add(ro, muls(rd, t)), F.blend, F.omblend, idl);
 #endif
     if (COUNT) {
       if (reflected) c.reflect++;
@@ -103,7 +104,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     hit = d < 0.000001f * t;
     dl = d;
     bool stop = hit | (d > tmax) | (i >= nmax);
-    t = stop ? t : t + d;
+    t += stop ? 0.0f : d;  // t >= +0: t + 0 == t
     if (RM_MISS_EXIT) {
       const bool gone = !stop && lin_exit(mx, t);
       if (COUNT) proven_miss |= gone;
@@ -114,7 +115,11 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   if (hit) {
     // the opU id (and colour) of the hit: from the last step's sdf (same point)
     const f3 q = add(ro, muls(rd, t));
+#if RM_LAZY_CULL
+    id = lazy_id(lc, t);
+#else
     id = idl;
+#endif
     col = hit_color(id, q);
     if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
     dlast = dl;

@@ -368,6 +368,8 @@ struct LazyCull {
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
   float ro1;     // |ro|_1
+  float tb;      // t of the last step that entered the re-test block
+  int idb;       // the opU id found there
 };
 
 __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
@@ -381,6 +383,8 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(c.rdlen + rd.y) * (1.0f - 0x1p-16f);
   c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
+  c.tb = -1.0f;
+  c.idb = 7;
 }
 
 // RM_LAZY_WAVE: the block and each re-test are entered per wave (any lane
@@ -407,14 +411,18 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
 #define RM_LZ_BLOCK(c) (c)
 #endif
 
-// id: the opU id of the minimum (glsl:105,110-121), as scene_exact<true> gives
-// it: the primitives are taken in the reference's order with ties going to the
-// later one, the plane last; culled primitives are strictly above the minimum
-// and can neither win nor tie.
-__device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float blend,
-                                            float omblend, int& id) {
-  float m = p.y + 5.5f;  // plane, exact (glsl:85,121); running minimum
-  id = 7;
+// The opU id of the minimum (glsl:105,110-121), as scene_exact<true> gives it,
+// is lazy_id(): the primitives are taken in the reference's order with ties
+// going to the later one, the plane last; culled primitives are strictly above
+// the minimum and can neither win nor tie.  A step that skips the block has
+// only the plane left: id 7.  (The block records its id with the step's t; t
+// strictly increases along a march, so tb == t identifies the step.)
+// The point is p = ro + rd t (the march's q); only p.y is needed outside the
+// re-test block, so p.x / p.z are formed inside it.
+__device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc, float blend,
+                                            float omblend) {
+  const float py = ro.y + rd.y * t;
+  float m = py + 5.5f;  // plane, exact (glsl:85,121); running minimum
   RM_STAT(8);
   if (RM_LZ_BLOCK(t >= lc.temin)) {
     const float plane = m;
@@ -447,6 +455,7 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
       te = expired ? tn : __builtin_fmaxf(te, tn);
       return expired & !(g > 0.0f);
     };
+    const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
     if (RM_LZ_ANY(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
@@ -484,10 +493,12 @@ __device__ __forceinline__ float scene_lazy(f3 p, float t, LazyCull& lc, float b
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
-    id = (plane <= mp) ? 7 : idp;
+    lc.idb = (plane <= mp) ? 7 : idp;
+    lc.tb = t;
   }
   return m;
 }
+__device__ __forceinline__ int lazy_id(const LazyCull& lc, float t) { return lc.tb == t ? lc.idb : 7; }
 
 #ifndef RM_SCENE_CULL
 #define RM_SCENE_CULL 1
