@@ -18,7 +18,12 @@ Rank 0 prints ONE JSON line.  Extra objects:
   roofline     : FP32-VALU roofline of the dominant kernel (k_sample / k_pixel);
                  achieved = algorithmic ops per launch (SURVEY 8(d) weights x the
                  exact work counters of the frames rendered) / mean kernel time
-                 measured with HIP events on the launch stream.
+                 measured with HIP events on the launch stream.  The algorithmic
+                 count is the reference's brute-force work (every primitive at
+                 every step); the kernel skips most of it by proof (culling,
+                 early exits), so `executed_valu_frac` (committed PMC
+                 SQ_INSTS_VALU x 64 lanes / time vs the lane-instruction peak)
+                 states how busy the VALU actually is.
   cpu_baseline : the CPU oracle (a C restatement of the reference shader) on
                  this host's cores, on a bounded row sample of the same frame;
                  its rows are also compared with the GPU frame (parity).
@@ -69,9 +74,10 @@ def algorithmic_ops(c: dict) -> int:
             + OPS["light"] * c["lights"] + OPS["ray"] * c["rays"])
 
 
-def pmc_traffic(kernel_name: str, workload: str):
-    """HBM bytes per launch of `kernel_name` from the newest committed PMC summary
-    (profiles/rNN_pmc.json, FETCH_SIZE/WRITE_SIZE passes of tools/profile_round.sh)."""
+def pmc_entry(kernel_name: str, workload: str):
+    """Per-launch PMC values of `kernel_name` from the newest committed summary
+    (profiles/rNN_pmc.json, separate rocprofv3 passes of tools/profile_round.sh:
+    FETCH_SIZE / WRITE_SIZE -> HBM bytes, SQ_INSTS_VALU -> executed VALU)."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         try:
@@ -82,7 +88,7 @@ def pmc_traffic(kernel_name: str, workload: str):
             continue
         for k, v in d.items():
             if kernel_name in k and "hbm_bytes_per_launch" in v:
-                return int(v["hbm_bytes_per_launch"]), os.path.basename(path)
+                return v, os.path.basename(path)
     return None, None
 
 
@@ -218,7 +224,12 @@ def main() -> int:
             cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
     mean_kernel_ms = kernel_ms / max(launches, 1)
     kname = ("k_sample" if cfg["aa"] else "k_pixel") if args.kernel == "pixel" else "k_wavequeue"
-    traffic, traffic_src = pmc_traffic(kname + "<false>", f"cfg{args.config}")
+    pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}")
+    traffic = int(pmc["hbm_bytes_per_launch"]) if pmc else None
+    # executed VALU issue rate: wave64 VALU instructions x 64 lanes / time, against
+    # the lane-instruction peak (157.3 TFLOP/s counts an FMA as 2 -> 78.65 T/s)
+    valu_insts = pmc.get("SQ_INSTS_VALU") if pmc else None
+    valu_issue = (valu_insts * 64 / (mean_kernel_ms * 1e-3) / 1e12) if valu_insts else None
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
     bytes_per_launch = r.rows * W * 4
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
@@ -274,6 +285,9 @@ def main() -> int:
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
                          "ops_per_launch": int(ops_total / max(launches, 1)),
+                         "executed_valu_Tlane_ops": round(valu_issue, 3) if valu_issue else None,
+                         "executed_valu_frac": (round(valu_issue / (VALU_PEAK_TFLOPS / 2), 4)
+                                                if valu_issue else None),
                          "hbm_write_GBs": round(hbm_gbs, 2),
                          "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
             "work": cnt_total,

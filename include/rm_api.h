@@ -172,11 +172,11 @@ int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
 
 /* ---- hipGraph frame replay (BASELINE cfg 5) ------------------------------ */
 /* rm_graph_enable(ctx, 1) switches the context to graph replay: the first
- * rm_graph_dispatch captures [copy of the frame constants from pinned host
- * memory to the device; render kernel reading them] into two double-buffered
- * graph instances; every later rm_graph_dispatch writes the current uniforms
- * to pinned memory and replays a graph on the context's stream (re-captured
- * only when AA toggles, which changes the grid).  Same image as rm_dispatch.
+ * rm_graph_dispatch captures the render-kernel launch into a graph; every
+ * later rm_graph_dispatch writes the current frame constants into the kernel
+ * node's by-value argument (hipGraphExecKernelNodeSetParams) and replays the
+ * graph on the context's stream (re-captured only when AA toggles, which
+ * changes the grid and kernel).  Same kernel and image as rm_dispatch.
  * Not available with cfg.counters or RM_KERNEL_WAVEQUEUE. */
 int rm_graph_enable(rm_ctx *ctx, int enable);
 int rm_graph_dispatch(rm_ctx *ctx);

@@ -24,17 +24,14 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s);
-hipError_t launch_pixel_dev(const rmd::Frame& F, const rmd::Frame* dF, hipStream_t s);
 }  // namespace rm
 
-// One double-buffer slot of the graph path: pinned host + device frame
-// constants and the instantiated graph that copies and renders them.
+// The graph path: one captured render-kernel node whose by-value frame
+// constants are replaced per frame (hipGraphExecKernelNodeSetParams).
 struct rm_graph_slot {
-  rmd::Frame* h = nullptr;
-  rmd::Frame* d = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphNode_t node = nullptr;
   hipGraphExec_t exec = nullptr;
-  hipEvent_t done = nullptr;
-  bool used = false;
 };
 
 struct rm_ctx {
@@ -59,8 +56,7 @@ struct rm_ctx {
   int64_t launches = 0;
   bool graph_on = false;
   int graph_aa = -1;  // AA value the graphs were captured for (grid shape depends on it)
-  int graph_next = 0;
-  rm_graph_slot gs[2];
+  rm_graph_slot gs;
   std::string err;
 };
 
@@ -136,14 +132,11 @@ rmd::Frame make_frame(const rm_ctx* c) {
 }
 
 void graph_release(rm_ctx* c) {
-  for (auto& g : c->gs) {
-    if (g.done) (void)hipEventSynchronize(g.done);
-    if (g.exec) (void)hipGraphExecDestroy(g.exec);
-    if (g.done) (void)hipEventDestroy(g.done);
-    if (g.h) (void)hipHostFree(g.h);
-    if (g.d) (void)hipFree(g.d);
-    g = rm_graph_slot();
-  }
+  rm_graph_slot& g = c->gs;
+  if (g.exec || g.graph) (void)hipStreamSynchronize(c->stream);
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g = rm_graph_slot();
   c->graph_aa = -1;
 }
 
@@ -471,52 +464,35 @@ int rm_read_sdf_counts(rm_ctx* c, uint32_t* dst) {
 }
 
 // ---- hipGraph frame replay -----------------------------------------------------------
-// Captures (once per AA setting) [H2D copy of the frame constants from pinned
-// host memory -> device, render kernel reading them] into two graph instances
-// with their own constant buffers, so the host can fill frame f+1's constants
-// while frame f renders.  rm_graph_dispatch replays one; nothing is captured per
-// frame.  Counters and the wave-queue kernel are not available on this path.
+// Captures (once per AA setting: the grid and kernel depend on it) the render
+// kernel launch into a graph.  Each rm_graph_dispatch writes the frame's
+// constants into the kernel node's by-value argument and replays it; the
+// kernel is the same code as rm_dispatch's (k_sample / k_pixel), so the graph
+// path renders identical images at identical register budgets.  Counters and
+// the wave-queue kernel are not available on this path.
 static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   graph_release(c);
+  rm_graph_slot& g = c->gs;
   hipStream_t cs = nullptr;
   RM_HIP(c, hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   int rc = RM_OK;
-  for (auto& g : c->gs) {
-    hipError_t e;
-    if ((e = hipHostMalloc(&g.h, sizeof(rmd::Frame), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipMalloc(&g.d, sizeof(rmd::Frame))) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&g.done, hipEventDisableTiming)) != hipSuccess) {
-      rc = hip_fail(c, e, "graph buffers");
-      break;
-    }
-    *g.h = F;
-    hipGraph_t graph = nullptr;
-    if ((e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal)) != hipSuccess) {
-      rc = hip_fail(c, e, "hipStreamBeginCapture");
-      break;
-    }
-    hipError_t e1 = hipMemcpyAsync(g.d, g.h, sizeof(rmd::Frame), hipMemcpyHostToDevice, cs);
-    hipError_t e2 = rm::launch_pixel_dev(F, g.d, cs);
-    e = hipStreamEndCapture(cs, &graph);
-    if (e1 != hipSuccess || e2 != hipSuccess || e != hipSuccess) {
-      rc = hip_fail(c, e1 != hipSuccess ? e1 : (e2 != hipSuccess ? e2 : e), "graph capture");
-      if (graph) (void)hipGraphDestroy(graph);
-      break;
-    }
-    e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (e != hipSuccess) {
-      rc = hip_fail(c, e, "hipGraphInstantiate");
-      break;
-    }
+  hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  if (e == hipSuccess) {
+    const hipError_t e1 = rm::launch_pixel(F, false, cs);
+    e = hipStreamEndCapture(cs, &g.graph);
+    if (e == hipSuccess) e = e1;
   }
+  size_t n = 1;
+  if (e == hipSuccess) e = hipGraphGetNodes(g.graph, &g.node, &n);
+  if (e == hipSuccess && n != 1) e = hipErrorInvalidValue;
+  if (e == hipSuccess) e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
   (void)hipStreamDestroy(cs);
-  if (rc != RM_OK) {
+  if (e != hipSuccess) {
+    rc = hip_fail(c, e, "graph capture");
     graph_release(c);
     return rc;
   }
   c->graph_aa = F.aa;
-  c->graph_next = 0;
   return RM_OK;
 }
 
@@ -541,12 +517,15 @@ int rm_graph_dispatch(rm_ctx* c) {
   if (!c->graph_on) return fail(c, RM_ERR_STATE, "rm_graph_enable(ctx, 1) first");
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
-  const rmd::Frame F = make_frame(c);
+  rmd::Frame F = make_frame(c);
   if (F.aa != c->graph_aa && (rc = graph_capture(c, F)) != RM_OK) return rc;
-  rm_graph_slot& g = c->gs[c->graph_next];
-  c->graph_next ^= 1;
-  if (g.used) RM_HIP(c, hipEventSynchronize(g.done));  // its constants were consumed
-  *g.h = F;
+  rm_graph_slot& g = c->gs;
+  hipKernelNodeParams kp;
+  RM_HIP(c, hipGraphKernelNodeGetParams(g.node, &kp));
+  void* args[] = {&F};
+  kp.kernelParams = args;
+  kp.extra = nullptr;
+  RM_HIP(c, hipGraphExecKernelNodeSetParams(g.exec, g.node, &kp));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     if (c->ev_used == c->ev_pool.size()) {
@@ -562,8 +541,6 @@ int rm_graph_dispatch(rm_ctx* c) {
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   RM_HIP(c, hipGraphLaunch(g.exec, c->stream));
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
-  RM_HIP(c, hipEventRecord(g.done, c->stream));
-  g.used = true;
   c->dispatched = true;
   return RM_OK;
 }

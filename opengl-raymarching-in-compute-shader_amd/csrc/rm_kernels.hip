@@ -416,17 +416,9 @@ template <bool COUNT>
 __global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
   pixel_body<COUNT>(F);
 }
-__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel_dev(const Frame* __restrict__ pF) {
-  const Frame F = *pF;
-  pixel_body<false>(F);
-}
 template <bool COUNT>
 __global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
   sample_body<COUNT>(F);
-}
-__global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample_dev(const Frame* __restrict__ pF) {
-  const Frame F = *pF;
-  sample_body<false>(F);
 }
 
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
@@ -465,19 +457,6 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
     hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(256), 0, s, F);
   else
     hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(256), 0, s, F);
-  return hipGetLastError();
-}
-
-// Graph-path launch: frame constants read from device memory (no counters).
-hipError_t launch_pixel_dev(const rmd::Frame& F, const rmd::Frame* dF, hipStream_t s) {
-  if (F.aa) {
-    const dim3 g((F.width + rmd::kSampleTile - 1) / rmd::kSampleTile,
-                 (F.rows + rmd::kSampleTile - 1) / rmd::kSampleTile);
-    hipLaunchKernelGGL(rmd::k_sample_dev, g, dim3(256), 0, s, dF);
-  } else {
-    const dim3 g((F.width + rmd::kTile - 1) / rmd::kTile, (F.rows + rmd::kTile - 1) / rmd::kTile);
-    hipLaunchKernelGGL(rmd::k_pixel_dev, g, dim3(256), 0, s, dF);
-  }
   return hipGetLastError();
 }
 

@@ -239,3 +239,23 @@ def test_graph_refuses_counters(rm, gpu):
     with rm.Renderer(32, 32, counters=True) as r:
         with pytest.raises(rm.RMError):
             r.graph_enable(True)
+
+
+def test_graph_back_to_back_frames_keep_their_constants(rm, gpu):
+    """Frames replayed back to back without host syncs, each into its own
+    output buffer: the per-frame constants set on the graph's kernel node must
+    not leak into a launch still in flight."""
+    import torch
+    W, H, n = 320, 180, 6
+    outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(n)]
+    us = [rm.sweep_uniforms(10 * f, 120, 3, True, 0) for f in range(n)]
+    with rm.Renderer(W, H) as g:
+        g.graph_enable(True)
+        for f in range(n):
+            g.set_output_rgba8(outs[f].data_ptr())
+            g.graph_dispatch(us[f])
+        g.synchronize()
+    with rm.Renderer(W, H) as r:
+        for f in range(n):
+            r.dispatch(us[f])
+            np.testing.assert_array_equal(outs[f].cpu().numpy(), r.read_rgba8(), err_msg=f"frame {f}")

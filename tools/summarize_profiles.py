@@ -24,7 +24,7 @@ def pmc(d):
     return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in per.items()}
 
 
-def main(src, tag, dst="profiles"):
+def main(src, tag, workload="cfg3", dst="profiles"):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -46,13 +46,16 @@ def main(src, tag, dst="profiles"):
             cs["hbm_read_bytes_corrected"] = 2 * f
             cs["hbm_write_bytes"] = w
             cs["hbm_bytes_per_launch"] = 2 * f + w
+    # bench.py matches a summary to its workload through _meta
+    out["_meta"] = {"workload": workload, "source": os.path.basename(os.path.normpath(src)),
+                    "passes": "separate rocprofv3 --pmc runs of tools/prof_kernels.py pixel 3 3"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     log = open(os.path.join(src, "bench_traced.log")).read().splitlines()
     line = [l for l in log if l.startswith("{")]
     if line:
         open(os.path.join(dst, f"{tag}_bench_traced.json"), "w").write(line[-1] + "\n")
-    print("wrote", dst, tag, list(out))
+    print("wrote", dst, tag, [k for k in out if k != "_meta"])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
