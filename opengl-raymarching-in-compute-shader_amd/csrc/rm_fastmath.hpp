@@ -14,20 +14,57 @@ constexpr float CAP_BAX = 2.0f - CAP_AX, CAP_BAY = 4.0f - CAP_AY, CAP_BAZ = 2.0f
 constexpr float CAP_BB_HOST = (CAP_BAX * CAP_BAX + CAP_BAY * CAP_BAY) + CAP_BAZ * CAP_BAZ;
 constexpr float CAP_BB_RCP = 1.0f / CAP_BB_HOST;  // correctly rounded reciprocal
 
-// Core of the correctly-rounded sqrt without the denormal pre-scale:
-// v_sqrt_f32 (within one ulp) and the one-ulp neighbour correction.
-// Exhaustively equal to __builtin_sqrtf for x == 0 and x in [2^-96, FLT_MAX];
-// callers route x in (0, 2^-96) to sqrt_cr_nonneg.
+// Correctly-rounded sqrt on {0} U [2^-96, FLT_MAX] in six instructions:
+// v_rsq_f32 and one Newton step (s = x y, r = x - s^2, s + (y/2) r), the way
+// the reciprocal-sqrt-based lowerings do it, proven bit-exact on every input of
+// that domain by tools/exhaustive_fp.hip.  The 2^-126 added before the rsq
+// vanishes in RN for x >= 2^-96 (ulp(x) >= 2^-119) and keeps x = 0 finite:
+// y = 2^63, s = 0, result exactly 0.  On (0, 2^-96) the result stays in
+// [0, 2^-47) (also checked exhaustively), so RN(sqrt_core(x) - R) = -R for the
+// radii R in {3, 2.5, 1, 0.5} it is always used with.  NaN stays NaN.
 __device__ __forceinline__ float sqrt_core(float x) {
-  float s = __builtin_amdgcn_sqrtf(x);
-  const int si = __float_as_int(s);
-  const float sm = __int_as_float(si - 1);
-  const float sp = __int_as_float(si + 1);
-  const float rm = __builtin_fmaf(-sm, s, x);
-  const float rp = __builtin_fmaf(-sp, s, x);
-  s = (rm <= 0.0f) ? sm : s;
-  s = (rp > 0.0f) ? sp : s;
-  return s;
+  const float y = __builtin_amdgcn_rsqf(x + 0x1p-126f);
+  const float s = x * y;
+  const float h = 0.5f * y;
+  const float r = __builtin_fmaf(-s, s, x);
+  return __builtin_fmaf(h, r, s);
+}
+
+// (RM_FAST_RCP, default off: measured no faster than the IEEE division here)
+// 1/x correctly rounded: v_rcp_f32 and one Newton step, proven bit-exact by
+// tools/exhaustive_fp.hip for every 2^-125 <= |x| <= 2^125; 0, inf, NaN and the
+// extreme magnitudes take the IEEE division (a rarely-taken branch).
+#ifndef RM_FAST_RCP
+#define RM_FAST_RCP 0
+#endif
+__device__ __forceinline__ float rcp_exact(float x) {
+  if (!RM_FAST_RCP) return 1.0f / x;
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  float r = __builtin_fmaf(e, y, y);
+  const float ax = fabsf(x);
+  if (!(ax >= 0x1p-125f && ax <= 0x1p125f)) r = 1.0f / x;
+  return r;
+}
+
+// x / i for the bounce weights, i = 1..5 (glsl:186-187, i wave-uniform): powers
+// of two are exact multiplies; 3 and 5 use the Markstein sequence with the
+// correctly rounded reciprocal (as div_capbb), proven bit-exact over all finite
+// x, signed zeros included, by tools/exhaustive_fp.hip.  Other i (not reachable)
+// divide.
+__device__ __forceinline__ float div_small(float x, int i) {
+  if (!RM_FAST_RCP) return x / (float)i;
+  if (i == 1) return x;
+  if (i == 2) return x * 0.5f;
+  if (i == 4) return x * 0.25f;
+  if (i == 3 || i == 5) {
+    const float d = (float)i;
+    const float y = (i == 3) ? (1.0f / 3.0f) : (1.0f / 5.0f);
+    const float q = x * y;
+    const float r = __builtin_fmaf(-q, d, x);
+    return q == 0.0f ? q : __builtin_fmaf(r, y, q);  // keeps -0 / 3 == -0
+  }
+  return x / (float)i;
 }
 
 // Smallest input sqrt_core handles exactly (besides 0).

@@ -231,10 +231,10 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     RM_PT(6, tcol.x);
     if (id == 7 && !prevMatte && i < 3) {
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
-      color = muls(color, sh / (float)i);
+      color = muls(color, div_small(sh, i));
     }
     RM_PT(7, color.x);
-    color = add(color, divs(mul(tcol, prevColor), (float)i));
+    color = add(color, divi(mul(tcol, prevColor), i));
     prevColor = tcol;
     prevMatte = (id == 7);  // material of the hit: MATTE only for the floor; dummy is 1.0
   }

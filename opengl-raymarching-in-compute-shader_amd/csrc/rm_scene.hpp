@@ -32,10 +32,12 @@ __device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, 
 __device__ __forceinline__ f3 subs(f3 a, float s) { return mk(a.x - s, a.y - s, a.z - s); }
 __device__ __forceinline__ f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+// a / i for the bounce weights (rm_fastmath.hpp div_small), exact
+__device__ __forceinline__ f3 divi(f3 a, int i) { return mk(div_small(a.x, i), div_small(a.y, i), div_small(a.z, i)); }
 // sqrt_cr_nonneg == the correctly rounded sqrt on [0, FLT_MAX] (rm_fastmath.hpp),
 // with NaN and +inf passing through unchanged
 __device__ __forceinline__ float len(f3 a) { return sqrt_cr_nonneg(dot(a, a)); }
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, 1.0f / sqrt_cr_nonneg(dot(a, a))); }
+__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_exact(sqrt_cr_nonneg(dot(a, a)))); }
 // v_min_f32 / v_min3_f32 without the NaN-quieting canonicalisations LLVM adds
 // when it cannot prove an operand canonical (values merged from branches).
 // All operands here are finite sdf values or +inf, never NaN.
@@ -629,7 +631,7 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
   float spec = gpow(gmax(dot(viewDir, reflectDir), 0.0f), 32.0f);
   f3 specular = muls(mk(F.lspec[0], F.lspec[1], F.lspec[2]), spec);
   float distance = len(sub(lpos, pos));
-  float attenuation = 1.0f / ((F.lconst + F.llin * distance) + F.lquad * (distance * distance));
+  float attenuation = rcp_exact((F.lconst + F.llin * distance) + F.lquad * (distance * distance));
   diffuse = muls(diffuse, attenuation);
   ambient = muls(ambient, attenuation);
   specular = muls(specular, attenuation);
@@ -649,7 +651,7 @@ __device__ __forceinline__ void cast_ray(const Frame& F, float uvx, float uvy, f
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = (uvx * F.cam_x[k] + uvy * F.cam_y[k]) + F.cam_dir[k] * F.persp;
   float dd = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-  float inv = 1.0f / sqrt_cr_nonneg(dd);
+  float inv = rcp_exact(sqrt_cr_nonneg(dd));
   ro = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
   rd = mk(v[0] * inv, v[1] * inv, v[2] * inv);
 }

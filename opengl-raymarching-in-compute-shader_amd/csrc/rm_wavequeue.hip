@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
             if (COUNT) c_light++;
             tc = point_light(F, id_color(hid, hchk), nrm, pos);
           }
-          const f3 term = divs(mul(tc, pcol), (float)bi);
+          const f3 term = divi(mul(tc, pcol), bi);
           if (hid == 7 && bi < 3) {
             pcol = term;  // stash: added after the shadow scales `color`
             ro = add(pos, muls(nrm, 0.02f));
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_wavequeue(WQFrame W) {
           if (bi == 0) {
             col = muls(col, res);  // glsl:237
           } else {
-            col = muls(col, res / (float)bi);  // glsl:186
+            col = muls(col, div_small(res, bi));  // glsl:186
             col = add(col, pcol);              // t.color * prevColor / i (glsl:192)
           }
           add_sample(col);

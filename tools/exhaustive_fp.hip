@@ -82,6 +82,90 @@ __global__ void k_div(unsigned long long* bad, unsigned* first) {
   }
 }
 
+// Direction of raw v_sqrt_f32's error on [2^-96, FLT_MAX]: counts of inputs where
+// the correctly rounded result is s (exact), s - 1 ulp (overshoot), s + 1 ulp
+// (undershoot), or further away.  One-sided errors allow a one-fma correction.
+__global__ void k_sqrt_dir(unsigned long long* cnt) {
+  const unsigned long long lo = 0x0f800000ull, n = 0x7f800000ull;  // 2^-96 .. FLT_MAX
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (unsigned long long i = lo + (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const float x = __uint_as_float((unsigned)i);
+    const int d = (int)__float_as_uint(__builtin_sqrtf(x)) - (int)__float_as_uint(__builtin_amdgcn_sqrtf(x));
+    c[d == 0 ? 0 : d == -1 ? 1 : d == 1 ? 2 : 3]++;
+  }
+  for (int k = 0; k < 4; ++k) atomicAdd(&cnt[k], c[k]);
+}
+
+// Candidate cheaper exact sqrt sequences, counted against the CR sqrt on [2^-96, max].
+__device__ __forceinline__ float cand_rsq_newton(float x) {  // rsq, s = x y, one Newton step
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s = x * y;
+  const float h = 0.5f * y;
+  const float r = __builtin_fmaf(-s, s, x);
+  return __builtin_fmaf(h, r, s);
+}
+__device__ __forceinline__ float cand_sqrt_newton(float x) {  // v_sqrt, residual, rcp step
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float r = __builtin_fmaf(-s, s, x);
+  return __builtin_fmaf(r, 0.5f * __builtin_amdgcn_rcpf(s), s);
+}
+__global__ void k_sqrt_cand(unsigned long long* cnt, unsigned* first) {
+  const unsigned long long lo = 0x0f800000ull, n = 0x7f800000ull;
+  unsigned long long c[2] = {0, 0};
+  for (unsigned long long i = lo + (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const float x = __uint_as_float((unsigned)i);
+    const unsigned ref = __float_as_uint(__builtin_sqrtf(x));
+    if (__float_as_uint(cand_rsq_newton(x)) != ref) { c[0]++; atomicMin(&first[0], (unsigned)i); }
+    if (__float_as_uint(cand_sqrt_newton(x)) != ref) { c[1]++; atomicMin(&first[1], (unsigned)i); }
+  }
+  atomicAdd(&cnt[0], c[0]);
+  atomicAdd(&cnt[1], c[1]);
+}
+
+// 1/x candidate: v_rcp_f32 plus one Newton step, against the IEEE division.
+__device__ __forceinline__ float cand_rcp_newton(float x) {
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+}
+__global__ void k_rcp_cand(unsigned long long* cnt, unsigned* first) {
+  unsigned long long c[2] = {0, 0};
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < 0x100000000ull;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const unsigned u = (unsigned)i;
+    if ((u & 0x7f800000u) == 0x7f800000u || (u & 0x7fffffffu) == 0) continue;  // inf/nan/0
+    const float x = __uint_as_float(u);
+    volatile float one = 1.0f;
+    const unsigned ref = __float_as_uint(one / x);
+    const int reg = (fabsf(x) >= 0x1p-125f && fabsf(x) <= 0x1p125f) ? 0 : 1;
+    if (__float_as_uint(cand_rcp_newton(x)) != ref) {
+      c[reg]++;
+      atomicMin(&first[reg], u & 0x7fffffffu);
+    }
+  }
+  atomicAdd(&cnt[0], c[0]);
+  atomicAdd(&cnt[1], c[1]);
+}
+
+// x / 3 and x / 5 (bounce weights 1/i, glsl:186-187) by the Markstein sequence
+// of div_small, against the IEEE division, over all finite x.
+__global__ void k_div_small(unsigned long long* cnt, unsigned* first) {
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < 0x100000000ull;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const unsigned u = (unsigned)i;
+    if ((u & 0x7f800000u) == 0x7f800000u) continue;
+    const float x = __uint_as_float(u);
+    volatile float d3 = 3.0f, d5 = 5.0f;
+    const int reg = fabsf(x) >= 0x1p-100f ? 0 : 1;
+    if (__float_as_uint(rmd::div_small(x, 3)) != __float_as_uint(x / d3)) { c[reg]++; atomicMin(&first[reg], u & 0x7fffffffu); }
+    if (__float_as_uint(rmd::div_small(x, 5)) != __float_as_uint(x / d5)) { c[2 + reg]++; atomicMin(&first[2 + reg], u & 0x7fffffffu); }
+  }
+  for (int k = 0; k < 4; ++k) atomicAdd(&cnt[k], c[k]);
+}
+
 int main() {
   unsigned long long* bad;
   unsigned* first;
@@ -101,6 +185,37 @@ int main() {
   printf("sqrt  sqrt_core on (0,2^-96) outside [0,2^-47): %llu (first 0x%08x)\n", hb[3], hf[3]);
   const bool sqrt_ok = hb[1] == 0 && hb[2] == 0 && hb[3] == 0;
   CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_sqrt_dir, dim3(4096), dim3(256), 0, 0, bad);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
+  printf("sqrt  v_sqrt_f32 on [2^-96,max]: exact %llu, over by 1ulp %llu, under by 1ulp %llu, other %llu\n",
+         hb[0], hb[1], hb[2], hb[3]);
+  CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
+  CK(hipMemset(first, 0xff, 4 * sizeof(unsigned)));
+  hipLaunchKernelGGL(k_sqrt_cand, dim3(4096), dim3(256), 0, 0, bad, first);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hf, first, sizeof hf, hipMemcpyDeviceToHost));
+  printf("sqrt  candidate rsq+Newton on [2^-96,max] mismatches: %llu (first 0x%08x)\n", hb[0], hf[0]);
+  printf("sqrt  candidate sqrt+rcp Newton on [2^-96,max] mismatches: %llu (first 0x%08x)\n", hb[1], hf[1]);
+  CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
+  CK(hipMemset(first, 0xff, 4 * sizeof(unsigned)));
+  hipLaunchKernelGGL(k_rcp_cand, dim3(4096), dim3(256), 0, 0, bad, first);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hf, first, sizeof hf, hipMemcpyDeviceToHost));
+  printf("rcp   candidate rcp+Newton 1/x on 2^-125<=|x|<=2^125 mismatches: %llu (first |x| 0x%08x)\n", hb[0], hf[0]);
+  printf("rcp   candidate rcp+Newton 1/x outside that range mismatches: %llu (first |x| 0x%08x)\n", hb[1], hf[1]);
+  CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
+  CK(hipMemset(first, 0xff, 4 * sizeof(unsigned)));
+  hipLaunchKernelGGL(k_div_small, dim3(4096), dim3(256), 0, 0, bad, first);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hf, first, sizeof hf, hipMemcpyDeviceToHost));
+  printf("div   div_small x/3 mismatches |x|>=2^-100: %llu, |x|<2^-100: %llu (first |x| 0x%08x)\n", hb[0], hb[1], hf[1]);
+  printf("div   div_small x/5 mismatches |x|>=2^-100: %llu, |x|<2^-100: %llu (first |x| 0x%08x)\n", hb[2], hb[3], hf[3]);
+  const bool small_ok = hb[0] == 0 && hb[1] == 0 && hb[2] == 0 && hb[3] == 0;
+  CK(hipMemset(bad, 0, 4 * sizeof(unsigned long long)));
   CK(hipMemset(first, 0xff, 2 * sizeof(unsigned)));
   CK(hipMemset(first + 2, 0, 2 * sizeof(unsigned)));
   hipLaunchKernelGGL(k_div, dim3(4096), dim3(256), 0, 0, bad, first);
@@ -112,5 +227,5 @@ int main() {
   printf("div   x/CAP_BB div_capbb mismatches |x|>=2^-100: %llu (|x| bits 0x%08x..0x%08x)\n",
          hb[1], hf[1], hf[3]);
   printf("div   |x|<2^-100: results not tiny or sign-flipped: %llu\n", hb[2]);
-  return (sqrt_ok && hb[1] == 0 && hb[2] == 0) ? 0 : 1;
+  return (sqrt_ok && small_ok && hb[1] == 0 && hb[2] == 0) ? 0 : 1;
 }
