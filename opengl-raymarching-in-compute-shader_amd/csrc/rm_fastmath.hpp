@@ -72,22 +72,14 @@ constexpr float SQRT_CORE_MIN = 0x1p-96f;
 // Smallest |x| for which div_capbb is exact.
 constexpr float DIV_CAPBB_MIN = 0x1p-100f;
 
-// sqrt(x) for x >= 0 (finite), correctly rounded.  v_sqrt_f32 plus the
-// one-ulp neighbour correction of the compiler's own lowering, with the
-// denormal pre-scale kept (x < 2^-96) but without the inf/nan class fixup
-// (not in the domain).  Exhaustively equal to __builtin_sqrtf on [0, FLT_MAX].
+// sqrt(x) for x >= 0 (finite), correctly rounded on all of [0, FLT_MAX]:
+// inputs below 2^-96 are scaled by 2^64 into sqrt_core's exact domain (the
+// smallest denormal becomes 2^-85) and the result by 2^-32 (both exact).  Exhaustively equal to __builtin_sqrtf on
+// [0, FLT_MAX] (tools/exhaustive_fp.hip).
 __device__ __forceinline__ float sqrt_cr_nonneg(float x) {
   const bool small = x < 0x1p-96f;
-  const float xs = small ? x * 0x1p32f : x;
-  float s = __builtin_amdgcn_sqrtf(xs);
-  const int si = __float_as_int(s);
-  const float sm = __int_as_float(si - 1);
-  const float sp = __int_as_float(si + 1);
-  const float rm = __builtin_fmaf(-sm, s, xs);
-  const float rp = __builtin_fmaf(-sp, s, xs);
-  s = (rm <= 0.0f) ? sm : s;
-  s = (rp > 0.0f) ? sp : s;
-  return small ? s * 0x1p-16f : s;
+  const float s = sqrt_core(small ? x * 0x1p64f : x);
+  return small ? s * 0x1p-32f : s;
 }
 
 // x / CAP_BB correctly rounded, as a multiply by the correctly-rounded
