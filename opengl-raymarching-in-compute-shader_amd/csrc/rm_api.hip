@@ -30,7 +30,8 @@ hipError_t launch_unshard(const void* gathered, void* frame, int width, int heig
 // constants are replaced per frame (hipGraphExecKernelNodeSetParams).
 struct rm_graph_slot {
   hipGraph_t graph = nullptr;
-  hipGraphNode_t node = nullptr;
+  hipGraphNode_t node[4] = {};  // the kernel nodes (k_prep, render), all taking a Frame
+  size_t nodes = 0;
   hipGraphExec_t exec = nullptr;
 };
 
@@ -48,6 +49,7 @@ struct rm_ctx {
   uint32_t* d_counts = nullptr;
   unsigned long long* d_counters = nullptr;
   uint32_t* d_queue = nullptr;
+  float* d_prep = nullptr;        // k_prep's per-frame step-0 values (rm_scene.hpp PrepSlot)
   bool dispatched = false;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -128,6 +130,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
   F.queue = c->d_queue;
+  F.prep = c->d_prep;
   return F;
 }
 
@@ -147,6 +150,7 @@ void free_all(rm_ctx* c) {
   if (c->d_counts) (void)hipFree(c->d_counts);
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_queue) (void)hipFree(c->d_queue);
+  if (c->d_prep) (void)hipFree(c->d_prep);
   for (auto& p : c->ev_pool) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
@@ -158,6 +162,7 @@ void free_all(rm_ctx* c) {
   c->d_counts = nullptr;
   c->d_counters = nullptr;
   c->d_queue = nullptr;
+  c->d_prep = nullptr;
   c->stream = nullptr;
 }
 
@@ -253,6 +258,8 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
       return bail(hip_fail(c, e, "hipMalloc counters"));
   }
   if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
+  if ((e = hipMalloc(&c->d_prep, 64)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc prep"));
+  if ((e = hipMemsetAsync(c->d_prep, 0, 64, c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipStreamSynchronize"));
   rm_default_uniforms(&c->u);
   // Tuning knobs of the wave-queue kernel; defaults are the tuned values.
@@ -482,9 +489,10 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
     e = hipStreamEndCapture(cs, &g.graph);
     if (e == hipSuccess) e = e1;
   }
-  size_t n = 1;
-  if (e == hipSuccess) e = hipGraphGetNodes(g.graph, &g.node, &n);
-  if (e == hipSuccess && n != 1) e = hipErrorInvalidValue;
+  size_t n = 4;
+  if (e == hipSuccess) e = hipGraphGetNodes(g.graph, g.node, &n);
+  if (e == hipSuccess && (n < 1 || n > 4)) e = hipErrorInvalidValue;
+  g.nodes = n;
   if (e == hipSuccess) e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
   (void)hipStreamDestroy(cs);
   if (e != hipSuccess) {
@@ -520,12 +528,14 @@ int rm_graph_dispatch(rm_ctx* c) {
   rmd::Frame F = make_frame(c);
   if (F.aa != c->graph_aa && (rc = graph_capture(c, F)) != RM_OK) return rc;
   rm_graph_slot& g = c->gs;
-  hipKernelNodeParams kp;
-  RM_HIP(c, hipGraphKernelNodeGetParams(g.node, &kp));
   void* args[] = {&F};
-  kp.kernelParams = args;
-  kp.extra = nullptr;
-  RM_HIP(c, hipGraphExecKernelNodeSetParams(g.exec, g.node, &kp));
+  for (size_t k = 0; k < g.nodes; ++k) {
+    hipKernelNodeParams kp;
+    RM_HIP(c, hipGraphKernelNodeGetParams(g.node[k], &kp));
+    kp.kernelParams = args;
+    kp.extra = nullptr;
+    RM_HIP(c, hipGraphExecKernelNodeSetParams(g.exec, g.node[k], &kp));
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     if (c->ev_used == c->ev_pool.size()) {

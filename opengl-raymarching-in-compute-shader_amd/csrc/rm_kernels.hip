@@ -20,6 +20,9 @@
 #ifndef RM_MISS_EXIT
 #define RM_MISS_EXIT 1
 #endif
+#ifndef RM_PRIMARY_PREP
+#define RM_PRIMARY_PREP 1
+#endif
 
 namespace rmd {
 
@@ -80,15 +83,38 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // with NaN should the ray hit after all (parity tests compare NaN masks)
   const float mx = miss_exit_init(ro, rd);
   bool proven_miss = false;
+  int i0 = 1;
+#if RM_LAZY_CULL && RM_PRIMARY_PREP
+  // Primary rays: step 0 is at the camera for every pixel; k_prep evaluated it
+  // once (its distance is exact, its bounds as the block would form them).
+  // Each lane only turns the bounds into expiries with its own |rd|: the
+  // re-test of scene_lazy with U = d0 (<= the block's running minimum).
+  if (!reflected && F.prep[PREP_VALID] != 0.0f) {
+    const float d0 = F.prep[PREP_D0], sl = F.prep[PREP_SLACK], pl = F.prep[PREP_PL];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float lb = F.prep[PREP_LB + k];
+      const float g = lb - d0 - sl;
+      const float bud = __builtin_fmaxf(g * lc.inv2v, (lb - pl) * lc.invp);
+      lc.te[k] = (g > 0.0f) ? 0.0f + bud : 0.0f;
+    }
+    lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
+    if (COUNT) c.march++;
+    dl = d0;
+    t = d0;
+    i0 = 2;
+  }
+#endif
   // One exit per step (hit | escape | step cap | proven miss), tested with
   // VALU: a single exec-mask update per iteration.
-  for (int i = 1;; ++i) {
+  for (int i = i0;; ++i) {
 #ifdef RM_STATS
     {
       const unsigned long long m = __ballot(1);
       if (__lane_id() == __builtin_ffsll(m) - 1) {
         atomicAdd(&g_stats[reflected ? 6 : 15], 1ull);
         atomicAdd(&g_stats[7], (unsigned long long)__popcll(m));
+        atomicAdd(&g_stats[16 + (reflected ? 6 : 15)], (unsigned long long)__popcll(m));
       }
     }
 #endif
@@ -421,6 +447,33 @@ __global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
   sample_body<COUNT>(F);
 }
 
+// Step 0 of the primary rays, once per frame (see PrepSlot, rm_scene.hpp).
+// The same device code as scene_lazy's first step at p = camera: the
+// distance is scene_exact's value (the exact minimum), the bounds are the
+// re-test's fma(v_sqrt(|p - c|^2), LO, -(ABS + R)).
+__global__ __launch_bounds__(64) void k_prep(Frame F) {
+  if (threadIdx.x != 0) return;
+  const f3 p = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
+  int id;
+  const float d0 = scene_exact<true>(p, F.blend, F.omblend, id);
+  const Offs o = offsets(p);
+  const float ro1 = fabsf(p.x) + fabsf(p.y) + fabsf(p.z);
+  const float sl = 0x1p-14f * (ro1 + 0.0f + 64.0f);
+  const float tz = p.z - 10.0f;
+  const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
+  const float x[5] = {(o.ax * o.ax + o.ay2) + o.az2, (o.bx * o.bx + o.ay2) + o.az2,
+                      (o.cx2 + o.ay2) + o.az2, (o.cx2 + o.ay2) + tz * tz,
+                      (kx * kx + ky * ky) + kz * kz};
+  const float R[5] = {3.0f, 3.0f, R_BLEND_LO, R_TORUS, R_CAPSULE};
+  float* out = const_cast<float*>(F.prep);
+  out[PREP_VALID] = (d0 > 0.0f && d0 <= 400.0f) ? 1.0f : 0.0f;
+  out[PREP_D0] = d0;
+  out[PREP_SLACK] = sl;
+  out[PREP_PL] = (p.y + 5.5f) + sl;
+  for (int k = 0; k < 5; ++k)
+    out[PREP_LB + k] = __builtin_fmaf(__builtin_amdgcn_sqrtf(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+}
+
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
@@ -443,6 +496,7 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
 namespace rm {
 
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
+  hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
   if (F.aa) {
     const dim3 g((F.width + rmd::kSampleTile - 1) / rmd::kSampleTile,
                  (F.rows + rmd::kSampleTile - 1) / rmd::kSampleTile);

@@ -76,6 +76,7 @@ struct Frame {
   uint32_t* sdf_counts;  // [rows][width] or null (counter builds)
   unsigned long long* counters;  // 6 x u64 (counter builds)
   uint32_t* queue;       // work-queue head (wave-queue kernel), zeroed per dispatch
+  const float* prep;     // step 0 of the primary rays (PrepSlot), written by k_prep
 };
 
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
@@ -372,6 +373,18 @@ struct LazyCull {
   float ro1;     // |ro|_1
   float tb;      // t of the last step that entered the re-test block
   int idb;       // the opU id found there
+};
+
+// Step 0 of every primary ray is the same computation: castRay starts all of
+// them at the camera (glsl:68-74) and p(0) = ro + rd*0 = ro exactly.  k_prep
+// runs it once per frame and leaves these values for the render kernel:
+enum PrepSlot : int {
+  PREP_VALID = 0,   // 1 when 0 < d0 <= 400 (no hit or escape at step 0)
+  PREP_D0 = 1,      // sdf(camera), the step-0 distance (exact, same ops as scene_lazy)
+  PREP_SLACK = 2,   // slack(0) of scene_lazy at the camera
+  PREP_PL = 3,      // plane(camera) + slack(0)
+  PREP_LB = 4,      // 5 lower bounds LB_k(camera), as scene_lazy's re-test forms them
+  PREP_COUNT = 9
 };
 
 __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {

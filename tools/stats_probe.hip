@@ -21,7 +21,8 @@ int main(int argc, char** argv) {
   printf("%-24s %12s %14s %6s\n", "point", "waves", "lanes", "lanes/wave");
   for (int k = 0; k < 16; ++k)
     printf("%-24s %12llu %14llu %6.1f\n", nm[k], h[k], h[16 + k], h[k] ? (double)h[16 + k] / h[k] : 0.0);
-  printf("march lane utilisation %.3f\n", (double)h[7] / (64.0 * (h[6] + h[15])));
+  printf("march lane utilisation %.3f (primary %.3f, reflected %.3f)\n", (double)h[7] / (64.0 * (h[6] + h[15])),
+         (double)h[31] / (64.0 * h[15]), (double)h[22] / (64.0 * h[6]));
   printf("lazy block rate: waves %.3f lanes %.3f\n", (double)h[9] / h[8], (double)h[25] / h[24]);
   rm_destroy(c);
   return 0;
