@@ -112,6 +112,9 @@ def main() -> int:
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: replay the frame from a captured hipGraph (rm_graph_dispatch); "
                          "default: on for config 5 (BASELINE 'hipGraph-captured frame')")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="N > 1: gather frame f on a second stream while frame f+1 renders "
+                         "(double-buffered shard images); 0 = render, gather, assemble in turn")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=4,
                     help="cpu_baseline renders every k-th row of one frame")
@@ -153,11 +156,26 @@ def main() -> int:
         r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
                         row_block=R, shard=rank, nshards=ws)
         rows_cap = r.rows
-        shard_buf = torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
-        r.set_output_rgba8(shard_buf.data_ptr())
+        nbuf = 2 if args.pipeline else 1
+        shard_bufs = [torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
+                      for _ in range(nbuf)]
+        r.set_output_rgba8(shard_bufs[0].data_ptr())
         gathered = (torch.empty((ws, rows_cap, W, 4), dtype=torch.uint8, device="cuda")
                     if rank == 0 else None)
         frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
+        # Pipelined: the gather (RCCL over xGMI) and the on-device assembly of frame f
+        # run on `comm` while frame f+1 renders on `stream`; events order each shard
+        # buffer's render -> gather -> next render.
+        comm = torch.cuda.Stream()
+        render_done = [torch.cuda.Event() for _ in range(nbuf)]
+        gather_done = [torch.cuda.Event() for _ in range(nbuf)]
+        for ev in gather_done:
+            ev.record(comm)
+        ru = None
+        if rank == 0:  # assembles on the comm stream (same shard geometry as r)
+            ru = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
+                             row_block=R, shard=0, nshards=ws)
+            ru.set_stream(comm.cuda_stream if args.pipeline else stream.cuda_stream)
     else:
         r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local)
         frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
@@ -166,16 +184,34 @@ def main() -> int:
     if use_graph:
         r.graph_enable(True)
 
-    def step(f):
+    def render(f):
         if use_graph:
             r.graph_dispatch(uniforms(f))
         else:
             r.dispatch(uniforms(f))
-        if ws > 1:
-            glist = list(gathered.unbind(0)) if rank == 0 else None
-            dist.gather(shard_buf, gather_list=glist, dst=0)
+
+    def step(f):
+        if ws == 1:
+            render(f)
+            return
+        glist = list(gathered.unbind(0)) if rank == 0 else None
+        if not args.pipeline:
+            render(f)
+            dist.gather(shard_bufs[0], gather_list=glist, dst=0)
             if rank == 0:
-                r.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
+                ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
+            return
+        j = f % 2
+        stream.wait_event(gather_done[j])        # buffer j's previous gather is done
+        r.set_output_rgba8(shard_bufs[j].data_ptr())
+        render(f)
+        render_done[j].record(stream)
+        with torch.cuda.stream(comm):
+            comm.wait_event(render_done[j])
+            dist.gather(shard_bufs[j], gather_list=glist, dst=0)
+            if rank == 0:
+                ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
+            gather_done[j].record(comm)
 
     def barrier():
         torch.cuda.synchronize()
@@ -277,6 +313,7 @@ def main() -> int:
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
                        "kernel": kname, "hipgraph": bool(use_graph),
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
+                                       + (" (pipelined)" if args.pipeline else "")
                                        if ws > 1 else "single GPU")},
             "fps": round(frames / elapsed, 3),
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3),
