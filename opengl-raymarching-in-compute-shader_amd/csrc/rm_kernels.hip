@@ -457,8 +457,7 @@ __global__ __launch_bounds__(64) void k_prep(Frame F) {
   int id;
   const float d0 = scene_exact<true>(p, F.blend, F.omblend, id);
   const Offs o = offsets(p);
-  const float ro1 = fabsf(p.x) + fabsf(p.y) + fabsf(p.z);
-  const float sl = 0x1p-14f * (ro1 + 0.0f + 64.0f);
+  const float sl = lazy_slack0(p);
   const float tz = p.z - 10.0f;
   const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
   const float x[5] = {(o.ax * o.ax + o.ay2) + o.az2, (o.bx * o.bx + o.ay2) + o.az2,

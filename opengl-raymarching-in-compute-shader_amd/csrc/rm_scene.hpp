@@ -367,10 +367,9 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
-  float rdlen;   // |rd| (rounded up)
+  float s0, s1;  // slack(t) = s0 + s1 t >= 2^-14 (|ro|_1 + |rd| t + 64)  (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
-  float ro1;     // |ro|_1
   float tb;      // t of the last step that entered the re-test block
   int idb;       // the opU id found there
 };
@@ -387,17 +386,23 @@ enum PrepSlot : int {
   PREP_COUNT = 9
 };
 
+// slack(0) at ray origin ro (also k_prep's): 2^-14 (|ro|_1 + 64), rounded up
+__device__ __forceinline__ float lazy_slack0(f3 ro) {
+  return 0x1p-14f * ((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z) + 64.0f) * (1.0f + 0x1p-20f);
+}
+
 __device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
   const float NEG = -__builtin_huge_valf();
 #pragma unroll
   for (int k = 0; k < 5; ++k) c.te[k] = NEG;
   c.temin = NEG;
-  c.rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);
-  c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(c.rdlen) * (1.0f - 0x1p-16f);
+  const float rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+  c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(rdlen) * (1.0f - 0x1p-16f);
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
-  c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(c.rdlen + rd.y) * (1.0f - 0x1p-16f);
-  c.ro1 = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z);
+  c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
+  c.s0 = lazy_slack0(ro);
+  c.s1 = 0x1p-14f * rdlen * (1.0f + 0x1p-20f);
   c.tb = -1.0f;
   c.idb = 7;
 }
@@ -445,7 +450,7 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     int idp = 7;
 
     RM_STAT(9);
-    const float slack = 0x1p-14f * (lc.ro1 + lc.rdlen * t + 64.0f);
+    const float slack = __builtin_fmaf(lc.s1, t, lc.s0);
     const float inv2v = lc.inv2v, invp = lc.invp;
     const float pl = m + slack;  // plane(p_i) + slack
     // an exactly evaluated k: its value bounds it like LB does (RM_LAZY_EXACT_TE),
@@ -464,10 +469,12 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       RM_STAT(1);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       const float g = lb - m - slack;
-      const float bud = __builtin_fmaxf(g * inv2v, (lb - pl) * invp);
-      const float tn = (g > 0.0f) ? t + bud : t;
+      // g <= 0 makes both budgets <= 0 (plane >= m), so max(.., 0) is the
+      // "no budget" case; an expired te is <= t <= t + bud, so max(te, .)
+      // serves both the expired lane and the idle one
+      const float bud = __builtin_fmaxf(__builtin_fmaxf(g * inv2v, (lb - pl) * invp), 0.0f);
       const bool expired = t >= te;
-      te = expired ? tn : __builtin_fmaxf(te, tn);
+      te = __builtin_fmaxf(te, t + bud);
       return expired & !(g > 0.0f);
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
