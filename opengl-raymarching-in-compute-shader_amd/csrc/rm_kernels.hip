@@ -318,7 +318,15 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 // main glsl:291-344, one thread per pixel.  A 256-thread workgroup covers a
 // 16x16 pixel tile and each wave an 8x8 sub-tile, so the 64 rays of a wave
 // are spatially coherent (similar step counts, same culled primitives).
-constexpr int kTile = 16;
+// Workgroup of RM_PIXEL_BLOCK threads = 1, 2 or 4 waves of 8x8 pixels.  One-wave
+// workgroups keep the CUs fuller: a finished wave's slot is refilled at once
+// instead of waiting for its workgroup's slowest wave.
+#ifndef RM_PIXEL_BLOCK
+#define RM_PIXEL_BLOCK 64
+#endif
+constexpr int kPixelWaves = RM_PIXEL_BLOCK / 64;
+constexpr int kTileW = kPixelWaves >= 2 ? 16 : 8;
+constexpr int kTileH = kPixelWaves == 4 ? 16 : 8;
 #ifndef RM_PIXEL_MIN_WAVES
 #define RM_PIXEL_MIN_WAVES 5
 #endif
@@ -328,8 +336,8 @@ constexpr int kTile = 16;
 template <bool COUNT>
 __device__ __forceinline__ void pixel_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int px = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-  const int lrow = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+  const int px = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
+  const int lrow = blockIdx.y * kTileH + (wave >> 1) * 8 + (lane >> 3);
   if (px >= F.width || lrow >= F.rows) return;
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
@@ -384,13 +392,20 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
 // cumulative uv of glsl:311-332 with the same sequential float adds, and lane
 // s == 0 sums the samples in the reference's fixed order ((c0+c1)+c2)+c3 via
 // lane shuffles before the /4 (glsl:315-335).
-constexpr int kSampleTile = 8;  // 8x8 pixels per 256-thread workgroup
+// Workgroup of RM_SAMPLE_BLOCK threads = 1, 2 or 4 waves of 4x4 pixels x 4 samples
+// (one-wave workgroups by default, as for k_pixel: 7 % faster than four).
+#ifndef RM_SAMPLE_BLOCK
+#define RM_SAMPLE_BLOCK 64
+#endif
+constexpr int kSampleWaves = RM_SAMPLE_BLOCK / 64;
+constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : 4;
+constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : 4;
 template <bool COUNT>
 __device__ __forceinline__ void sample_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
-  const int px = blockIdx.x * kSampleTile + (wave & 1) * 4 + (q & 3);
-  const int lrow = blockIdx.y * kSampleTile + (wave >> 1) * 4 + (q >> 2);
+  const int px = blockIdx.x * kSampleTileW + (wave & 1) * 4 + (q & 3);
+  const int lrow = blockIdx.y * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
   if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
@@ -439,11 +454,11 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
 // through a device pointer (graph replay, rm_graph_dispatch: the graph copies
 // the per-frame constants from pinned host memory before the launch).
 template <bool COUNT>
-__global__ __launch_bounds__(256, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
+__global__ __launch_bounds__(RM_PIXEL_BLOCK, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
   pixel_body<COUNT>(F);
 }
 template <bool COUNT>
-__global__ __launch_bounds__(256, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
+__global__ __launch_bounds__(RM_SAMPLE_BLOCK, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
   sample_body<COUNT>(F);
 }
 
@@ -497,19 +512,19 @@ namespace rm {
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
   hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
   if (F.aa) {
-    const dim3 g((F.width + rmd::kSampleTile - 1) / rmd::kSampleTile,
-                 (F.rows + rmd::kSampleTile - 1) / rmd::kSampleTile);
+    const dim3 g((F.width + rmd::kSampleTileW - 1) / rmd::kSampleTileW,
+                 (F.rows + rmd::kSampleTileH - 1) / rmd::kSampleTileH);
     if (counters)
-      hipLaunchKernelGGL(rmd::k_sample<true>, g, dim3(256), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<true>, g, dim3(RM_SAMPLE_BLOCK), 0, s, F);
     else
-      hipLaunchKernelGGL(rmd::k_sample<false>, g, dim3(256), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<false>, g, dim3(RM_SAMPLE_BLOCK), 0, s, F);
     return hipGetLastError();
   }
-  const dim3 grid((F.width + rmd::kTile - 1) / rmd::kTile, (F.rows + rmd::kTile - 1) / rmd::kTile);
+  const dim3 grid((F.width + rmd::kTileW - 1) / rmd::kTileW, (F.rows + rmd::kTileH - 1) / rmd::kTileH);
   if (counters)
-    hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(256), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
   else
-    hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(256), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
   return hipGetLastError();
 }
 
