@@ -26,6 +26,9 @@
 
 namespace rmd {
 
+#ifdef RM_WAVE_TIMES
+__device__ unsigned long long* g_wave_times;
+#endif
 #ifdef RM_PHASE_TIMING
 // Diagnostic build only: wave clock cycles spent per phase (tools/phase_probe.hip).
 // RM_PT(k, v) charges the time since the previous mark to phase k once v (the
@@ -412,6 +415,9 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   Cnt c = {0, 0, 0, 0, 0, 0};
   f3 col = mk(0.0f, 0.0f, 0.0f);
   RM_PT_BEGIN();
+#ifdef RM_WAVE_TIMES
+  const unsigned long long wt0 = wall_clock64();
+#endif
   if (py >= 0) {
     float x = (float)(px * 2 - F.width) / (float)F.width;
     float y = (float)(py * 2 - F.height) / (float)F.height;
@@ -439,6 +445,17 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
     atomicAdd(&F.counters[5], (unsigned long long)c.lights);
   }
   RM_PT(8, col.x);
+#ifdef RM_WAVE_TIMES
+  // diagnostic (tools/wave_timeline.hip): per-wave start/end and hardware slot
+  if (lane == 0) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const size_t w = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    g_wave_times[3 * w] = wt0;
+    g_wave_times[3 * w + 1] = wall_clock64();
+    g_wave_times[3 * w + 2] = hw;
+  }
+#endif
   if (s != 0) return;
   if (py >= 0) {
     const float o0 = ((col.x + r1) + r2) + r3, o1 = ((col.y + g1) + g2) + g3,

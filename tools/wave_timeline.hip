@@ -1,0 +1,86 @@
+// Diagnostic: per-wave lifetimes of one cfg-3 k_sample launch (RM_WAVE_TIMES):
+// concurrency over time (waves alive / 8 per SIMD), dispatch gaps, tail.
+#define RM_WAVE_TIMES 1
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_kernels.hip"
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_api.hip"
+#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_wavequeue.hip"
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+int main() {
+  const int W = 3840, H = 2160;
+  rm_config cfg = {W, H, 0, RM_OUT_RGBA8, RM_KERNEL_PIXEL, 0, 0, 0, 1};
+  rm_ctx* c;
+  if (rm_create(&c, &cfg)) return 1;
+  const size_t nw = (size_t)(W / 4) * (H / 4);
+  unsigned long long* d;
+  hipMalloc(&d, nw * 3 * 8);
+  hipMemset(d, 0, nw * 3 * 8);
+  hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_wave_times), &d, sizeof d);
+  rm_uniforms u;
+  rm_sweep_uniforms(30, 120, 3, 1, 0, &u);
+  rm_set_uniforms(c, &u);
+  rm_dispatch(c);  // warm
+  rm_synchronize(c);
+  rm_dispatch(c);
+  rm_synchronize(c);
+  std::vector<unsigned long long> h(nw * 3);
+  hipMemcpy(h.data(), d, nw * 3 * 8, hipMemcpyDeviceToHost);
+  unsigned long long t0 = ~0ull, t1 = 0;
+  for (size_t w = 0; w < nw; ++w) { t0 = std::min(t0, h[3 * w]); t1 = std::max(t1, h[3 * w + 1]); }
+  const double span = (double)(t1 - t0);  // wall_clock64 ticks (100 MHz)
+  printf("waves %zu, span %.1f us\n", nw, span / 100.0);
+  // concurrency histogram over 40 time bins
+  const int NB = 40;
+  std::vector<double> alive(NB, 0.0);
+  double life = 0;
+  for (size_t w = 0; w < nw; ++w) {
+    const double a = (double)(h[3 * w] - t0), b = (double)(h[3 * w + 1] - t0);
+    life += b - a;
+    for (int k = 0; k < NB; ++k) {
+      const double lo = span * k / NB, hi = span * (k + 1) / NB;
+      const double ov = std::max(0.0, std::min(b, hi) - std::max(a, lo));
+      alive[k] += ov / (hi - lo);
+    }
+  }
+  printf("mean wave life %.2f us; mean resident %.0f waves = %.2f per SIMD (1024 SIMDs)\n",
+         life / nw / 100.0, life / span, life / span / 1024.0);
+  for (int k = 0; k < NB; ++k) printf("bin %2d  %.2f waves/SIMD\n", k, alive[k] / 1024.0);
+  // per-slot gaps: group by hardware id (SE/SH/CU/SIMD/wave slot)
+  std::vector<std::pair<unsigned, std::pair<unsigned long long, unsigned long long>>> v;
+  for (size_t w = 0; w < nw; ++w) v.push_back({(unsigned)h[3 * w + 2], {h[3 * w], h[3 * w + 1]}});
+  std::sort(v.begin(), v.end());
+  double gap = 0; size_t ng = 0; std::vector<double> gaps;
+  for (size_t i = 1; i < v.size(); ++i)
+    if (v[i].first == v[i - 1].first && v[i].second.first >= v[i - 1].second.second) {
+      const double g = (double)(v[i].second.first - v[i - 1].second.second);
+      gap += g; ++ng; gaps.push_back(g);
+    }
+  std::sort(gaps.begin(), gaps.end());
+  if (ng) printf("slot refill gaps: %zu, mean %.2f us, median %.2f us, p90 %.2f us\n", ng, gap / ng / 100.0,
+                 gaps[ng / 2] / 100.0, gaps[ng * 9 / 10] / 100.0);
+  // the last waves to finish: their tile row / column and lifetime
+  std::vector<std::pair<unsigned long long, size_t>> ends;
+  for (size_t w = 0; w < nw; ++w) ends.push_back({h[3 * w + 1], w});
+  std::sort(ends.begin(), ends.end());
+  const size_t gx = W / 4;
+  printf("last 12 waves to finish (tile row of %d, col, start us, life us):\n", H / 4);
+  for (size_t i = nw - 12; i < nw; ++i) {
+    const size_t w = ends[i].second;
+    printf("  row %4zu col %4zu start %7.1f life %6.1f\n", w / gx, w % gx, (h[3 * w] - t0) / 100.0,
+           (h[3 * w + 1] - h[3 * w]) / 100.0);
+  }
+  // lifetime by tile-row band (10 bands)
+  for (int b = 0; b < 10; ++b) {
+    double s = 0, mx = 0; size_t n = 0;
+    for (size_t w = 0; w < nw; ++w) {
+      const size_t row = w / gx;
+      if (row * 10 / (H / 4) != (size_t)b) continue;
+      const double l = (h[3 * w + 1] - h[3 * w]) / 100.0;
+      s += l; mx = std::max(mx, l); ++n;
+    }
+    printf("rows band %d: mean life %.1f us, max %.1f us\n", b, s / n, mx);
+  }
+  rm_destroy(c);
+  return 0;
+}
