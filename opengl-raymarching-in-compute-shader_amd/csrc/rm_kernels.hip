@@ -336,6 +336,21 @@ __device__ __forceinline__ int tile_row(int b, int n) {
   return b;
 }
 
+// XCD-aware tile column: one-wave workgroups go round-robin to the 8 XCDs
+// (block b -> XCD b % 8), so consecutive blocks land in different L2s and the
+// 16-32 B row segments that neighbouring tiles store into one 128 B line are
+// written back separately (PMC: 2x write amplification).  Within each window of
+// 8 G blocks, XCD k takes the G adjacent tiles [k G, (k+1) G): a line's
+// segments meet in one L2, while the XCDs still interleave at G-tile grain
+// (a coarse split, XCD k = columns [k gx/8, ...), unbalanced the XCDs: 2x slower).
+__device__ __forceinline__ int tile_col(int b, int gx, int G) {
+  const int win = 8 * G;
+  const int w0 = (b / win) * win;
+  if (w0 + win > gx) return b;  // ragged last window: natural order
+  const int r = b - w0;
+  return w0 + (r & 7) * G + (r >> 3);
+}
+
 // main glsl:291-344, one thread per pixel.  A 256-thread workgroup covers a
 // 16x16 pixel tile and each wave an 8x8 sub-tile, so the 64 rays of a wave
 // are spatially coherent (similar step counts, same culled primitives).
@@ -358,7 +373,8 @@ template <bool COUNT>
 __device__ __forceinline__ void pixel_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int by = tile_row(blockIdx.y, gridDim.y);
-  const int px = blockIdx.x * kTileW + (wave & 1) * 8 + (lane & 7);
+  const int bx = tile_col(blockIdx.x, gridDim.x, 128 / (kTileW * 4));
+  const int px = bx * kTileW + (wave & 1) * 8 + (lane & 7);
   const int lrow = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
   if (px >= F.width || lrow >= F.rows) return;
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
@@ -427,7 +443,8 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
   const int by = tile_row(blockIdx.y, gridDim.y);
-  const int px = blockIdx.x * kSampleTileW + (wave & 1) * 4 + (q & 3);
+  const int bx = tile_col(blockIdx.x, gridDim.x, 128 / (kSampleTileW * 4));
+  const int px = bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
   const int lrow = by * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
   if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
@@ -470,7 +487,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   if (lane == 0) {
     unsigned hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    const size_t w = (size_t)by * gridDim.x + blockIdx.x;
+    const size_t w = (size_t)by * gridDim.x + bx;
     g_wave_times[3 * w] = wt0;
     g_wave_times[3 * w + 1] = wall_clock64();
     g_wave_times[3 * w + 2] = hw;
