@@ -77,14 +77,25 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   bool hit = false;
+  // per-ray constants; the ro-dependent ones of primary rays come from k_prep
+  const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
+  float s0, b1, b2;
+  if (RM_PRIMARY_PREP && !reflected && F.prep[PREP_VALID] != 0.0f) {
+    s0 = F.prep[PREP_SLACK];
+    b1 = F.prep[PREP_B1];
+    b2 = F.prep[PREP_B2];
+  } else {
+    s0 = ray_s0(ro);
+    lin_exit_b(ro, s0, 0.0f, b1, b2);
+  }
 #if RM_LAZY_CULL
   LazyCull lc;
-  lazy_init(lc, ro, rd);
+  lazy_init(lc, rd, rdl, s0, s1);
 #endif
   // provable miss (rm_scene.hpp "early exits"): production stops there; the
   // counting build runs on to the reference's step count and poisons the colour
   // with NaN should the ray hit after all (parity tests compare NaN masks)
-  const float mx = miss_exit_init(ro, rd);
+  const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
   bool proven_miss = false;
   int i0 = 1;
 #if RM_LAZY_CULL && RM_PRIMARY_PREP
@@ -526,7 +537,7 @@ __global__ __launch_bounds__(64) void k_prep(Frame F) {
   int id;
   const float d0 = scene_exact<true>(p, F.blend, F.omblend, id);
   const Offs o = offsets(p);
-  const float sl = lazy_slack0(p);
+  const float sl = ray_s0(p);
   const float tz = p.z - 10.0f;
   const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
   const float x[5] = {(o.ax * o.ax + o.ay2) + o.az2, (o.bx * o.bx + o.ay2) + o.az2,
@@ -538,6 +549,10 @@ __global__ __launch_bounds__(64) void k_prep(Frame F) {
   out[PREP_D0] = d0;
   out[PREP_SLACK] = sl;
   out[PREP_PL] = (p.y + 5.5f) + sl;
+  float b1, b2;
+  lin_exit_b(p, sl, 0.0f, b1, b2);
+  out[PREP_B1] = b1;
+  out[PREP_B2] = b2;
   for (int k = 0; k < 5; ++k)
     out[PREP_LB + k] = __builtin_fmaf(__builtin_amdgcn_sqrtf(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
 }

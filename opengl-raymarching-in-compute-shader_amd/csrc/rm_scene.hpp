@@ -380,29 +380,39 @@ struct LazyCull {
 enum PrepSlot : int {
   PREP_VALID = 0,   // 1 when 0 < d0 <= 400 (no hit or escape at step 0)
   PREP_D0 = 1,      // sdf(camera), the step-0 distance (exact, same ops as scene_lazy)
-  PREP_SLACK = 2,   // slack(0) of scene_lazy at the camera
+  PREP_SLACK = 2,   // ray_s0(camera): slack(0) of scene_lazy at the camera
   PREP_PL = 3,      // plane(camera) + slack(0)
   PREP_LB = 4,      // 5 lower bounds LB_k(camera), as scene_lazy's re-test forms them
-  PREP_COUNT = 9
+  PREP_B1 = 9,      // lin_exit_b(camera, slack, 0): the miss exit's ro-dependent terms
+  PREP_B2 = 10,
+  PREP_COUNT = 11
 };
 
-// slack(0) at ray origin ro (also k_prep's): 2^-14 (|ro|_1 + 64), rounded up
-__device__ __forceinline__ float lazy_slack0(f3 ro) {
-  return 0x1p-14f * ((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z) + 64.0f) * (1.0f + 0x1p-20f);
+// Per-ray constants shared by the lazy culler and the linear exits: |rd| from
+// one v_sqrt (within 1.5 ulp) and the slack line s0 + s1 t, rounded up with
+// 2^-12 margins: s0 >= 2^-14 (|ro|_1 + 64), s1 >= 2^-14 |rd|.
+__device__ __forceinline__ float ray_rdl(f3 rd) { return __builtin_amdgcn_sqrtf(dot(rd, rd)); }
+__device__ __forceinline__ float ray_s0(f3 ro) {
+  const float HI = 1.0f + 0x1p-12f;
+  return 0x1p-14f * (((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z)) * HI + 64.0f) * HI;
+}
+__device__ __forceinline__ float ray_s1(float rdl) {
+  const float HI = 1.0f + 0x1p-12f;
+  return 0x1p-14f * rdl * (HI * HI);
 }
 
-__device__ __forceinline__ void lazy_init(LazyCull& c, f3 ro, f3 rd) {
+__device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s0, float s1) {
   const float NEG = -__builtin_huge_valf();
 #pragma unroll
   for (int k = 0; k < 5; ++k) c.te[k] = NEG;
   c.temin = NEG;
-  const float rdlen = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+  const float rdlen = rdl * (1.0f + 0x1p-16f);  // >= |rd|
   c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(rdlen) * (1.0f - 0x1p-16f);
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
-  c.s0 = lazy_slack0(ro);
-  c.s1 = 0x1p-14f * rdlen * (1.0f + 0x1p-20f);
+  c.s0 = s0;
+  c.s1 = s1;
   c.tb = -1.0f;
   c.idb = 7;
 }
@@ -558,33 +568,39 @@ __device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id
 // so the per-step test is one compare, t > T.
 constexpr float SH_CX = -5.0f, SH_CY = 0.0f, SH_CZ = -10.0f;
 constexpr float SH_RALL = 23.001f;  // >= max_k |C - c_k| + R_k = 20 + 3 (spheres, torus)
-__device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
-  const float LO = 1.0f - 0x1p-12f, HI = 1.0f + 0x1p-12f;
-  const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd));
-  const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
-  const float s0 = 0x1p-14f * (ro1 * HI + 64.0f) * HI;
-  const float s1 = 0x1p-14f * rdl * (HI * HI);
+// The ro-dependent half (b1, b2): uniform for primary rays, so k_prep forms it
+// once per frame (PREP_B1/B2); the rd-dependent half gives T per ray.
+__device__ __forceinline__ void lin_exit_b(f3 ro, float s0, float hmin, float& b1, float& b2) {
+  const float HI = 1.0f + 0x1p-12f;
   const float ex = ro.x - SH_CX, ey = ro.y - SH_CY, ez = ro.z - SH_CZ;
   const float rc = __builtin_fmaf(__builtin_amdgcn_sqrtf((ex * ex + ey * ey) + ez * ez), HI, 0x1p-18f);
+  b1 = (rc + SH_RALL + s0 + hmin) * HI;
+  b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
+}
+__device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float s1, float b1, float b2) {
+  const float LO = 1.0f - 0x1p-12f;
   // absolute 2^-20 terms: the rounding of a difference is relative to its
   // operands, not to a small (cancelled) result
   const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
-  const float b1 = (rc + SH_RALL + s0 + hmin) * HI;
-  const float a2 = (rd.y - s1 - c) * LO - 0x1p-20f * (fabsf(rd.y) + s1 + c);
-  const float b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
+  const float a2 = (rdy - s1 - c) * LO - 0x1p-20f * (fabsf(rdy) + s1 + c);
   const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
   const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * UP;
   const float T2 = -(b2 * __builtin_amdgcn_rcpf(a2) * (b2 >= 0.0f ? DN : UP));
   const float INF = __builtin_huge_valf();
   return (a1 > 0.0f && a2 > 0.0f) ? __builtin_fmaxf(T1, T2) : INF;
 }
+constexpr float MISS_C = 0.000001f * (1.0f + 0x1p-9f);
+__device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
+  const float rdl = ray_rdl(rd), s0 = ray_s0(ro);
+  float b1, b2;
+  lin_exit_b(ro, s0, hmin, b1, b2);
+  return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2);
+}
 __device__ __forceinline__ float shadow_exit_init(float k, f3 ro, f3 rd) {
   const float c = (k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / k * (1.0f + 0x1p-12f);
   return lin_exit_init(c, 0.001f, ro, rd);
 }
-__device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) {
-  return lin_exit_init(0.000001f * (1.0f + 0x1p-9f), 0.0f, ro, rd);
-}
+__device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd); }
 __device__ __forceinline__ bool lin_exit(float T, float t) { return t > T; }
 
 // softshadow's  res = min(res, k * h / t)  (glsl:211), exactly.  The quotient
