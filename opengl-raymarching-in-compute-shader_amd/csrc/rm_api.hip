@@ -50,6 +50,7 @@ struct rm_ctx {
   unsigned long long* d_counters = nullptr;
   uint32_t* d_queue = nullptr;
   float* d_prep = nullptr;        // k_prep's per-frame step-0 values (rm_scene.hpp PrepSlot)
+  float* d_uv = nullptr;          // per-column / per-row uv table (Frame::uvx / uvy)
   bool dispatched = false;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -110,13 +111,8 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.omblend = 1.0f - F.blend;
   F.k = (u.shadow_mode == RM_SHADOW_HARD) ? INFINITY : 2.0f;
   F.persp = 45.0f * static_cast<float>(0.01745329251994329576923690768489);
-  {
-    const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f}, oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
-    for (int k = 0; k < 4; ++k) {
-      F.aa_dx[k] = ox[k] / (float)c->cfg.width;
-      F.aa_dy[k] = oy[k] / (float)c->cfg.height;
-    }
-  }
+  F.uvx = c->d_uv;
+  F.uvy = c->d_uv + (size_t)5 * c->cfg.width;
   F.bounces = u.bounceVar;
   F.aa = u.AA ? 1 : 0;
   F.width = c->cfg.width;
@@ -151,6 +147,7 @@ void free_all(rm_ctx* c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->d_prep) (void)hipFree(c->d_prep);
+  if (c->d_uv) (void)hipFree(c->d_uv);
   for (auto& p : c->ev_pool) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
@@ -163,6 +160,7 @@ void free_all(rm_ctx* c) {
   c->d_counters = nullptr;
   c->d_queue = nullptr;
   c->d_prep = nullptr;
+  c->d_uv = nullptr;
   c->stream = nullptr;
 }
 
@@ -259,6 +257,26 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   }
   if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
   if ((e = hipMalloc(&c->d_prep, 64)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc prep"));
+  {
+    // uv of the pixel columns and rows with the shader's float operations
+    // (glsl:301-305 and the cumulative sub-sample offsets of :309-332)
+    const int W = c->cfg.width, H = c->cfg.height;
+    const float ox[4] = {0.25f, 0.75f, 0.25f, 0.75f}, oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
+    std::vector<float> uv((size_t)5 * (W + H));
+    for (int p = 0; p < W + H; ++p) {
+      const bool col = p < W;
+      const int i = col ? p : p - W, n = col ? W : H;
+      float v = (float)(i * 2 - n) / (float)n;
+      uv[(size_t)p * 5] = v;
+      for (int k = 0; k < 4; ++k) {
+        v += (col ? ox[k] : oy[k]) / (float)n;
+        uv[(size_t)p * 5 + 1 + k] = v;
+      }
+    }
+    if ((e = hipMalloc(&c->d_uv, uv.size() * sizeof(float))) != hipSuccess ||
+        (e = hipMemcpy(c->d_uv, uv.data(), uv.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+      return bail(hip_fail(c, e, "uv table"));
+  }
   if ((e = hipMemsetAsync(c->d_prep, 0, 64, c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipStreamSynchronize"));
   rm_default_uniforms(&c->u);

@@ -393,14 +393,11 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
   Cnt c = {0, 0, 0, 0, 0, 0};
   float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
   if (py >= 0) {
-    float x = (float)(px * 2 - F.width) / (float)F.width;
-    float y = (float)(py * 2 - F.height) / (float)F.height;
     f3 ro, rd;
     if (F.aa) {
 #pragma unroll 1
       for (int s = 0; s < 4; ++s) {
-        x += F.aa_dx[s];
-        y += F.aa_dy[s];
+        const float x = F.uvx[px * 5 + 1 + s], y = F.uvy[py * 5 + 1 + s];
         cast_ray(F, x, y, ro, rd);
         if (COUNT) c.rays++;
         f3 col = render<COUNT>(F, ro, rd, c);
@@ -413,7 +410,7 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
       o2 = o2 / 4.0f;
       o3 = 1.0f;
     } else {
-      cast_ray(F, x, y, ro, rd);
+      cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
       if (COUNT) c.rays++;
       f3 col = render<COUNT>(F, ro, rd, c);
       o0 = col.x;
@@ -467,14 +464,8 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   const unsigned long long wt0 = wall_clock64();
 #endif
   if (py >= 0) {
-    float x = (float)(px * 2 - F.width) / (float)F.width;
-    float y = (float)(py * 2 - F.height) / (float)F.height;
-    for (int j = 0; j <= s; ++j) {
-      x += F.aa_dx[j];
-      y += F.aa_dy[j];
-    }
     f3 ro, rd;
-    cast_ray(F, x, y, ro, rd);
+    cast_ray(F, F.uvx[px * 5 + 1 + s], F.uvy[py * 5 + 1 + s], ro, rd);
     if (COUNT) c.rays++;
     col = render<COUNT>(F, ro, rd, c);
   }

@@ -65,7 +65,11 @@ struct Frame {
   float omblend;   // 1 - blend (uniform-only subexpression of mix)
   float k;         // softshadow k: 2.0 (glsl:185,236) or +inf (hard-shadow extension)
   float persp;     // radians(45) = 45 * 0.017453292519943295f (glsl:70)
-  float aa_dx[4], aa_dy[4];  // offsetX[s] / dims.x, offsetY[s] / dims.y (glsl:311-332), host IEEE
+  // uv of every pixel column / row, host IEEE in the shader's order (glsl:301-332):
+  // [k = 0] (2 p - dims) / dims, [k = 1 + s] after the cumulative sub-sample
+  // offsets offset[0..s] / dims; 5 floats per column (uvx) and per row (uvy)
+  const float* uvx;
+  const float* uvy;
   int32_t bounces; // bounceVar, 0..5
   int32_t aa;      // AA
   int32_t width, height;
