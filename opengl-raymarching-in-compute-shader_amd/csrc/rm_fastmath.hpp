@@ -67,6 +67,16 @@ __device__ __forceinline__ float div_small(float x, int i) {
   return x / (float)i;
 }
 
+// 1/s for s = sqrt_cr_nonneg(d) of a finite d >= 0, i.e. s = 0 or
+// 2^-74.5 <= s <= 2^64, inside rcp_exact's proven range: no guard needed.  For
+// s = 0 (and NaN) it gives NaN where the IEEE 1/s gives inf; normalize()
+// multiplies that by the zero vector, and 0 * inf is NaN too.
+__device__ __forceinline__ float rcp_of_sqrt(float s) {
+  const float y = __builtin_amdgcn_rcpf(s);
+  const float e = __builtin_fmaf(-s, y, 1.0f);
+  return __builtin_fmaf(e, y, y);
+}
+
 // Smallest input sqrt_core handles exactly (besides 0).
 constexpr float SQRT_CORE_MIN = 0x1p-96f;
 // Smallest |x| for which div_capbb is exact.

@@ -37,7 +37,7 @@ __device__ __forceinline__ f3 divi(f3 a, int i) { return mk(div_small(a.x, i), d
 // sqrt_cr_nonneg == the correctly rounded sqrt on [0, FLT_MAX] (rm_fastmath.hpp),
 // with NaN and +inf passing through unchanged
 __device__ __forceinline__ float len(f3 a) { return sqrt_cr_nonneg(dot(a, a)); }
-__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_exact(sqrt_cr_nonneg(dot(a, a)))); }
+__device__ __forceinline__ f3 normalize(f3 a) { return muls(a, rcp_of_sqrt(sqrt_cr_nonneg(dot(a, a)))); }
 // v_min_f32 / v_min3_f32 without the NaN-quieting canonicalisations LLVM adds
 // when it cannot prove an operand canonical (values merged from branches).
 // All operands here are finite sdf values or +inf, never NaN.
@@ -691,7 +691,7 @@ __device__ __forceinline__ void cast_ray(const Frame& F, float uvx, float uvy, f
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = (uvx * F.cam_x[k] + uvy * F.cam_y[k]) + F.cam_dir[k] * F.persp;
   float dd = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-  float inv = rcp_exact(sqrt_cr_nonneg(dd));
+  float inv = rcp_of_sqrt(sqrt_cr_nonneg(dd));
   ro = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
   rd = mk(v[0] * inv, v[1] * inv, v[2] * inv);
 }
