@@ -112,6 +112,10 @@ def main() -> int:
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: replay the frame from a captured hipGraph (rm_graph_dispatch); "
                          "default: on for config 5 (BASELINE 'hipGraph-captured frame')")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="frames in flight: consecutive frames render from separate contexts on "
+                         "separate streams, so frame f+1's waves fill the SIMDs that frame f's "
+                         "last long waves leave idle (1 = one context, frames in turn)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="N > 1: gather frame f on a second stream while frame f+1 renders "
                          "(double-buffered shard images); 0 = render, gather, assemble in turn")
@@ -141,74 +145,75 @@ def main() -> int:
     if use_graph and kernel == rm.RM_KERNEL_WAVEQUEUE:
         print("bench.py: --graph renders with the default kernel", file=sys.stderr)
         return 2
-    # An explicit stream (torch's default stream has a NULL handle, which librm
-    # would replace by its own stream): librm's kernels and the RCCL gather are
-    # then ordered on one stream.
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
+    # Explicit streams (torch's default stream has a NULL handle, which librm would
+    # replace by its own stream): each in-flight context renders on its own stream;
+    # the RCCL gather and the assembly run on `comm`, ordered by events.
+    nfl = max(1, args.inflight) if (ws == 1 or args.pipeline) else 1
+    streams = [torch.cuda.Stream() for _ in range(nfl)]
+    torch.cuda.set_stream(streams[0])
 
     def uniforms(f):
         return rm.sweep_uniforms(f % SWEEP_FRAMES, SWEEP_FRAMES, cfg["bounces"], cfg["aa"],
                                  cfg["shadow"])
 
+    shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if ws > 1 else {}
+    rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
+          for _ in range(nfl)]
+    r = rs[0]
     if ws > 1:
         R = args.row_block
-        r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
-                        row_block=R, shard=rank, nshards=ws)
         rows_cap = r.rows
-        nbuf = 2 if args.pipeline else 1
-        shard_bufs = [torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
-                      for _ in range(nbuf)]
-        r.set_output_rgba8(shard_bufs[0].data_ptr())
+        nbuf = nfl if args.pipeline else 1
+        outs = [torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
+                for _ in range(nbuf)]
         gathered = (torch.empty((ws, rows_cap, W, 4), dtype=torch.uint8, device="cuda")
                     if rank == 0 else None)
         frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
-        # Pipelined: the gather (RCCL over xGMI) and the on-device assembly of frame f
-        # run on `comm` while frame f+1 renders on `stream`; events order each shard
-        # buffer's render -> gather -> next render.
         comm = torch.cuda.Stream()
-        render_done = [torch.cuda.Event() for _ in range(nbuf)]
-        gather_done = [torch.cuda.Event() for _ in range(nbuf)]
-        for ev in gather_done:
-            ev.record(comm)
         ru = None
         if rank == 0:  # assembles on the comm stream (same shard geometry as r)
             ru = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
                              row_block=R, shard=0, nshards=ws)
-            ru.set_stream(comm.cuda_stream if args.pipeline else stream.cuda_stream)
+            ru.set_stream(comm.cuda_stream if args.pipeline else streams[0].cuda_stream)
     else:
-        r = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local)
-        frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
-        r.set_output_rgba8(frame.data_ptr())
-    r.set_stream(stream.cuda_stream)
-    if use_graph:
-        r.graph_enable(True)
-
-    def render(f):
+        outs = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nfl)]
+    render_done = [torch.cuda.Event() for _ in range(nfl)]
+    gather_done = [torch.cuda.Event() for _ in range(nfl)]
+    if ws > 1:
+        for ev in gather_done:
+            ev.record(comm)
+    for j, rj in enumerate(rs):
+        rj.set_stream(streams[j].cuda_stream)
+        rj.set_output_rgba8(outs[j % len(outs)].data_ptr())
         if use_graph:
-            r.graph_dispatch(uniforms(f))
+            rj.graph_enable(True)
+
+    def render(j, f):
+        if use_graph:
+            rs[j].graph_dispatch(uniforms(f))
         else:
-            r.dispatch(uniforms(f))
+            rs[j].dispatch(uniforms(f))
 
     def step(f):
+        j = f % nfl
         if ws == 1:
-            render(f)
+            render(j, f)
             return
         glist = list(gathered.unbind(0)) if rank == 0 else None
         if not args.pipeline:
-            render(f)
-            dist.gather(shard_bufs[0], gather_list=glist, dst=0)
+            render(0, f)
+            dist.gather(outs[0], gather_list=glist, dst=0)
             if rank == 0:
                 ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
             return
-        j = f % 2
-        stream.wait_event(gather_done[j])        # buffer j's previous gather is done
-        r.set_output_rgba8(shard_bufs[j].data_ptr())
-        render(f)
-        render_done[j].record(stream)
+        # frame f renders on streams[j] into outs[j] once that buffer's previous
+        # gather is done; the gather and the assembly follow on `comm`
+        streams[j].wait_event(gather_done[j])
+        render(j, f)
+        render_done[j].record(streams[j])
         with torch.cuda.stream(comm):
             comm.wait_event(render_done[j])
-            dist.gather(shard_bufs[j], gather_list=glist, dst=0)
+            dist.gather(outs[j], gather_list=glist, dst=0)
             if rank == 0:
                 ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
             gather_done[j].record(comm)
@@ -225,16 +230,36 @@ def main() -> int:
     barrier()
 
     # ---- timed region: exactly K steps ----
-    r.enable_timing(True)
-    r.kernel_time_ms(reset=True)
+    for rj in rs:
+        rj.enable_timing(True)
+        rj.kernel_time_ms(reset=True)
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k)
     barrier()
     t1 = time.perf_counter()
-    kernel_ms, launches = r.kernel_time_ms(reset=True)
-    r.enable_timing(False)
+    kernel_ms, launches = 0.0, 0
+    for rj in rs:
+        ms_j, n_j = rj.kernel_time_ms(reset=True)
+        kernel_ms += ms_j
+        launches += n_j
+        rj.enable_timing(False)
+    kernel_time_basis = "HIP events on the launch stream over the timed region"
+    if nfl > 1:
+        # Overlapping frames stretch each launch's event interval, so the roofline
+        # takes its kernel time from the same frames rendered one at a time on one
+        # context (HIP events, untimed for `value`).
+        barrier()
+        r.enable_timing(True)
+        r.kernel_time_ms(reset=True)
+        for k in range(args.steps):
+            render(0, args.warmup + k)
+        barrier()
+        kernel_ms, launches = r.kernel_time_ms(reset=True)
+        r.enable_timing(False)
+        kernel_time_basis = ("HIP events, the timed frames re-rendered one at a time "
+                             "(the timed region overlaps frames)")
     elapsed = t1 - t0
     if ws > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -287,9 +312,9 @@ def main() -> int:
                "cores": threads, "kind": "port",
                "sample": f"rows py%{args.cpu_row_stride}==0 of sweep frame {f} "
                          f"({len(rows)}x{W} px, {cfg['desc']}), {c1 - c0:.2f}s wall"}
-        # GPU frame of the same sweep frame: the last step rendered it into `frame`.
+        # GPU frame of the same sweep frame: the last step rendered it into its context's buffer.
         torch.cuda.synchronize()
-        g = frame.cpu().numpy()[rows]
+        g = outs[(args.warmup + args.steps - 1) % nfl].cpu().numpy()[rows]
         d = np.abs(g.astype(np.int16) - ref["rgba8"].astype(np.int16))
         parity = {"max_abs_delta_rgba8": int(d.max()), "pixels_over_2": int((d.max(-1) > 2).sum()),
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
@@ -311,7 +336,7 @@ def main() -> int:
             "config": {"workload": f"cfg{args.config}: {cfg['desc']}", "width": W, "height": H,
                        "bounces": cfg["bounces"], "aa": cfg["aa"],
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
-                       "kernel": kname, "hipgraph": bool(use_graph),
+                       "kernel": kname, "hipgraph": bool(use_graph), "frames_in_flight": nfl,
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        + (" (pipelined)" if args.pipeline else "")
                                        if ws > 1 else "single GPU")},
@@ -321,6 +346,7 @@ def main() -> int:
                          "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
+                         "kernel_time_basis": kernel_time_basis,
                          "ops_per_launch": int(ops_total / max(launches, 1)),
                          "executed_valu_Tlane_ops": round(valu_issue, 3) if valu_issue else None,
                          "executed_valu_frac": (round(valu_issue / (VALU_PEAK_TFLOPS / 2), 4)
@@ -332,7 +358,8 @@ def main() -> int:
             "parity": parity,
         }
         print(json.dumps(out), flush=True)
-    r.close()
+    for rj in rs:
+        rj.close()
     if ws > 1:
         dist.destroy_process_group()
     return 0

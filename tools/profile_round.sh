@@ -9,7 +9,7 @@ set -e
 OUT=$1; shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/bench_traced.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --inflight 1 "$@" > "$OUT/bench_traced.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 tools/prof_kernels.py pixel 3 3 > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 tools/prof_kernels.py pixel 3 3 > "$OUT/write.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_TRANS_F32 SQ_BUSY_CYCLES -d "$OUT/sq" -o run --output-format csv -- python3 tools/prof_kernels.py pixel 3 3 > "$OUT/sq.log" 2>&1

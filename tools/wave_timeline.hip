@@ -7,12 +7,16 @@
 #include <algorithm>
 #include <cstdio>
 #include <vector>
-int main() {
+int main(int argc, char** argv) {
   const int W = 3840, H = 2160;
-  rm_config cfg = {W, H, 0, RM_OUT_RGBA8, RM_KERNEL_PIXEL, 0, 0, 0, 1};
+  const int nsh = argc > 1 ? atoi(argv[1]) : 1;  // optional: row-block shards (rank 0's shard)
+  rm_config cfg = {W, H, 0, RM_OUT_RGBA8, RM_KERNEL_PIXEL, 0, nsh > 1 ? 8 : 0, 0, nsh};
   rm_ctx* c;
   if (rm_create(&c, &cfg)) return 1;
-  const size_t nw = (size_t)(W / 4) * (H / 4);
+  int rows = H;
+  rm_shard_rows_cap(H, 8, nsh, &rows);
+  if (nsh <= 1) rows = H;
+  const size_t nw = (size_t)(W / 4) * ((rows + 3) / 4);
   unsigned long long* d;
   hipMalloc(&d, nw * 3 * 8);
   hipMemset(d, 0, nw * 3 * 8);
@@ -64,7 +68,7 @@ int main() {
   for (size_t w = 0; w < nw; ++w) ends.push_back({h[3 * w + 1], w});
   std::sort(ends.begin(), ends.end());
   const size_t gx = W / 4;
-  printf("last 12 waves to finish (tile row of %d, col, start us, life us):\n", H / 4);
+  printf("last 12 waves to finish (tile row of %d, col, start us, life us):\n", (rows + 3) / 4);
   for (size_t i = nw - 12; i < nw; ++i) {
     const size_t w = ends[i].second;
     printf("  row %4zu col %4zu start %7.1f life %6.1f\n", w / gx, w % gx, (h[3 * w] - t0) / 100.0,
@@ -75,7 +79,7 @@ int main() {
     double s = 0, mx = 0; size_t n = 0;
     for (size_t w = 0; w < nw; ++w) {
       const size_t row = w / gx;
-      if (row * 10 / (H / 4) != (size_t)b) continue;
+      if (row * 10 / ((rows + 3) / 4) != (size_t)b) continue;
       const double l = (h[3 * w + 1] - h[3 * w]) / 100.0;
       s += l; mx = std::max(mx, l); ++n;
     }
