@@ -112,10 +112,12 @@ def main() -> int:
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: replay the frame from a captured hipGraph (rm_graph_dispatch); "
                          "default: on for config 5 (BASELINE 'hipGraph-captured frame')")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames render from separate contexts on "
                          "separate streams, so frame f+1's waves fill the SIMDs that frame f's "
-                         "last long waves leave idle (1 = one context, frames in turn)")
+                         "last long waves leave idle (1 = one context, frames in turn; "
+                         "0 = 3 on one GPU, 4 on a sharded frame, whose per-rank share is "
+                         "shorter than its longest waves)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="N > 1: gather frame f on a second stream while frame f+1 renders "
                          "(double-buffered shard images); 0 = render, gather, assemble in turn")
@@ -148,7 +150,8 @@ def main() -> int:
     # Explicit streams (torch's default stream has a NULL handle, which librm would
     # replace by its own stream): each in-flight context renders on its own stream;
     # the RCCL gather and the assembly run on `comm`, ordered by events.
-    nfl = max(1, args.inflight) if (ws == 1 or args.pipeline) else 1
+    nfl = args.inflight if args.inflight > 0 else (3 if ws == 1 else 4)
+    nfl = nfl if (ws == 1 or args.pipeline) else 1
     streams = [torch.cuda.Stream() for _ in range(nfl)]
     torch.cuda.set_stream(streams[0])
 
