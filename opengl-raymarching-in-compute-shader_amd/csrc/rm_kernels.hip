@@ -121,8 +121,12 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #endif
   // One exit per step (hit | escape | step cap | proven miss), tested with
   // VALU: a single exec-mask update per iteration.
+#ifdef RM_STATS
+  int nst = 0;  // this lane's steps (diagnostic builds)
+#endif
   for (int i = i0;; ++i) {
 #ifdef RM_STATS
+    ++nst;
     {
       const unsigned long long m = __ballot(1);
       if (__lane_id() == __builtin_ffsll(m) - 1) {
@@ -152,6 +156,12 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     }
     if (stop) break;
   }
+#ifdef RM_STATS
+  // lane sums of steps: [4] primary miss, [5] primary hit, [20] reflected miss,
+  // [21] reflected hit; [12] / [13] count the primary miss / hit lanes
+  atomicAdd(&g_stats[(reflected ? 20 : 4) + (hit ? 1 : 0)], (unsigned long long)nst);
+  if (!reflected) atomicAdd(&g_stats[hit ? 13 : 12], 1ull);
+#endif
   if (hit) {
     // the opU id (and colour) of the hit: from the last step's sdf (same point)
     const f3 q = add(ro, muls(rd, t));

@@ -24,6 +24,9 @@ int main(int argc, char** argv) {
   printf("march lane utilisation %.3f (primary %.3f, reflected %.3f)\n", (double)h[7] / (64.0 * (h[6] + h[15])),
          (double)h[31] / (64.0 * h[15]), (double)h[22] / (64.0 * h[6]));
   printf("lazy block rate: waves %.3f lanes %.3f\n", (double)h[9] / h[8], (double)h[25] / h[24]);
+  printf("primary rays: %llu misses, %.1f steps each; %llu hits, %.1f steps each\n", h[12],
+         (double)h[4] / h[12], h[13], (double)h[5] / h[13]);
+  printf("reflected: steps of misses %llu, of hits %llu\n", h[20], h[21]);
   rm_destroy(c);
   return 0;
 }
