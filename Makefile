@@ -46,14 +46,19 @@ $(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h
 	@mkdir -p $(dir $@)
 	$(CC) $(OFLAGS) -shared -o $@ oracle/rm_oracle.c -lm
 
-$(DRIVER): $(PKG)/tools/rm_frameloop.cpp include/rm/camera.hpp include/rm/texture.hpp $(LIBRM)
+$(DRIVER): $(PKG)/tools/rm_frameloop.cpp include/rm/camera.hpp include/rm/input.hpp include/rm/texture.hpp $(LIBRM)
 	$(CXX) -std=c++17 -O2 -Wall -Iinclude -o $@ $< -L$(PKG) -lrm -Wl,-rpath,'$$ORIGIN'
 
 # Camera goldens from the reference's vendored GLM 0.9.8.5 (third-party, in
 # /root/reference/includes/glm).  Output binary only under oracle/_ref/.
 REF ?= /root/reference
-goldens: oracle/_ref/gen_camera_goldens
+goldens: oracle/_ref/gen_camera_goldens oracle/_ref/gen_input_goldens
 	oracle/_ref/gen_camera_goldens > tests/golden/camera_goldens.json
+	oracle/_ref/gen_input_goldens > tests/golden/input_goldens.json
+
+oracle/_ref/gen_input_goldens: oracle/gen_input_goldens.cpp
+	@mkdir -p oracle/_ref
+	$(CXX) -std=c++11 -O2 -ffp-contract=off -I$(REF)/includes -o $@ $<
 
 oracle/_ref/gen_camera_goldens: oracle/gen_camera_goldens.cpp
 	@mkdir -p oracle/_ref

@@ -42,7 +42,7 @@ class Camera {
     const float p[3] = {pos.x, pos.y, pos.z}, l[3] = {lookAt.x, lookAt.y, lookAt.z},
                 u[3] = {upv.x, upv.y, upv.z};
     rm_camera_init(&s, w, h, sens, speed, p, l, u);
-    load(s);
+    assign(s);
   }
 
   // camera.cpp:16-20
@@ -53,21 +53,21 @@ class Camera {
 
   // camera.cpp:22-51
   void lookAt(bool zN, bool zP, bool xN, bool xP, bool halfSpeed, float deltaTime) {
-    rm_camera_state s = store();
+    rm_camera_state s = state();
     rm_camera_look_at(&s, zN, zP, xN, xP, halfSpeed, deltaTime);
-    load(s);
+    assign(s);
   }
 
   // main.cpp:103-106 — the four setVec4("camera.*") uploads (w = 0)
   rm_camera toUniform() const {
     rm_camera c;
-    rm_camera_state s = store();
+    rm_camera_state s = state();
     rm_camera_to_uniform(&s, &c);
     return c;
   }
 
- private:
-  rm_camera_state store() const {
+  // The C-ABI view of this camera (rm_camera_state) and back, for rm_input_*.
+  rm_camera_state state() const {
     rm_camera_state s;
     s.width = width;
     s.height = height;
@@ -83,7 +83,7 @@ class Camera {
     put(s.right, right);
     return s;
   }
-  void load(const rm_camera_state& s) {
+  void assign(const rm_camera_state& s) {
     width = s.width;
     height = s.height;
     angleY = s.angleY;
@@ -97,6 +97,7 @@ class Camera {
     up = get(s.up);
     right = get(s.right);
   }
+ private:
   static void put(float* d, const vec3& v) {
     d[0] = v.x;
     d[1] = v.y;

@@ -231,6 +231,64 @@ int rm_camera_look_at(rm_camera_state *c, int zN, int zP, int xN, int xP, int ha
 /* The four setVec4 calls of main.cpp:103-106 (w = 0). */
 int rm_camera_to_uniform(const rm_camera_state *c, rm_camera *out);
 
+/* ---- interactive input mapping ------------------------
+ * The reference's GLFW input globals and callbacks (main.cpp:20-39, 93-95,
+ * 155-234; source/MousePosition.cpp:4-22) as a state struct and four event
+ * functions, so any windowing front-end can feed its key/mouse events and get
+ * the reference's camera motion, bounce/AA toggles and uniforms.  Key and
+ * action codes are GLFW's (glfw3.h) so a GLFW front-end passes them through. */
+#define RM_KEY_A 65
+#define RM_KEY_D 68
+#define RM_KEY_L 76
+#define RM_KEY_S 83
+#define RM_KEY_W 87
+#define RM_KEY_ESCAPE 256
+#define RM_KEY_DOWN 264
+#define RM_KEY_UP 265
+#define RM_KEY_F1 290
+#define RM_RELEASE 0
+#define RM_PRESS 1
+#define RM_REPEAT 2
+/* keys held this frame (glfwGetKey(...) == GLFW_PRESS), for rm_input_process */
+#define RM_HELD_W 1u
+#define RM_HELD_A 2u
+#define RM_HELD_S 4u
+#define RM_HELD_D 8u
+#define RM_HELD_ESCAPE 16u
+
+typedef struct rm_input_state {
+  int32_t zaxisPos, zaxisNeg, xaxisPos, xaxisNeg; /* main.cpp:23-26 */
+  int32_t AA;                                     /* main.cpp:27 (true) */
+  int32_t showQuad;                               /* main.cpp:28 wireframe toggle (display only) */
+  float halfSpeed;                                /* main.cpp:29 (a float in the reference) */
+  int32_t bounce;                                 /* main.cpp:30, 0..5 */
+  float deltaTime, lastFrame;                     /* main.cpp:32-33 */
+  float lastX, lastY;                             /* main.cpp:35-36 (screen centre) */
+  int32_t firstMouse;                             /* main.cpp:37 */
+  float pitch, yaw;                               /* MouseInput mouse, main.cpp:39 */
+  float mouseSensitivity;                         /* MouseSensitivity, MousePosition.hpp:8 */
+  int32_t shouldClose;                            /* glfwSetWindowShouldClose (main.cpp:157) */
+} rm_input_state;
+
+/* The globals' initial values for a screen_width x screen_height window. */
+int rm_input_init(rm_input_state *s, int32_t screen_width, int32_t screen_height);
+/* main.cpp:93-95: currentFrame = (float)now; deltaTime = currentFrame - lastFrame. */
+int rm_input_begin_frame(rm_input_state *s, double now_seconds);
+/* processInput  main.cpp:155-195: axis flags and halfSpeed from the held keys
+ * (RM_HELD_*), ESC -> shouldClose, then camera.lookAt(..., deltaTime). */
+int rm_input_process(rm_input_state *s, uint32_t held, rm_camera_state *cam);
+/* key_callback  main.cpp:197-217: UP/DOWN bounce within 0..5, F1 toggles AA,
+ * L toggles showQuad; only RM_PRESS acts (repeats are ignored). */
+int rm_input_key(rm_input_state *s, int32_t key, int32_t action);
+/* mouse_callback  main.cpp:219-234: MouseInput offsets, camera.setMouse(-x, -y). */
+int rm_input_mouse(rm_input_state *s, double xpos, double ypos, rm_camera_state *cam);
+/* MouseInput::EulerAngles  MousePosition.cpp:24-33 (the "mouse" uniform). */
+int rm_input_euler_angles(const rm_input_state *s, float out[3]);
+/* The per-frame uploads of main.cpp:101-120 that input drives: camera block,
+ * AA, bounceVar, mouse = EulerAngles(), iMouse = (yaw, pitch), and
+ * iTime = the frame's clock sample (lastFrame).  Other fields are untouched. */
+int rm_input_to_uniforms(const rm_input_state *s, const rm_camera_state *cam, rm_uniforms *u);
+
 /* ---- synthetic frames -------------------------------------- */
 /* Sweep S(F): camera at (0,0,15), yaw -20..+20 deg over F frames, pitch -5 deg,
  * iTime = f/60; lights of main.cpp:108-114. frame < 0 selects the default

@@ -186,6 +186,107 @@ int rm_camera_to_uniform(const rm_camera_state* c, rm_camera* out) {
   return RM_OK;
 }
 
+// ---- interactive input: main.cpp's GLFW globals/callbacks ----
+// The reference keeps this state in globals (main.cpp:23-39); here it is one
+// struct per front-end.  The float/double conversions follow the reference's
+// declared types exactly: lastX/lastY/deltaTime/lastFrame are float, GLFW hands
+// doubles to the callbacks, and halfSpeed is a float holding a bool.
+
+int rm_input_init(rm_input_state* s, int32_t screen_width, int32_t screen_height) {
+  if (!s || screen_width <= 0 || screen_height <= 0) return RM_ERR_INVALID;
+  std::memset(s, 0, sizeof(*s));
+  s->AA = 1;                                      // main.cpp:27
+  s->lastX = (float)(screen_width / 2.0);         // main.cpp:35 (SCREEN_WIDTH / 2.0)
+  s->lastY = (float)(screen_height / 2.0);        // main.cpp:36
+  s->firstMouse = 1;                              // main.cpp:37
+  s->mouseSensitivity = (float)0.001;             // MousePosition.hpp:8 (double literal -> float)
+  return RM_OK;                                   // pitch = yaw = 0: MousePosition.cpp:4-5
+}
+
+// main.cpp:93-95
+int rm_input_begin_frame(rm_input_state* s, double now_seconds) {
+  if (!s) return RM_ERR_INVALID;
+  const float currentFrame = (float)now_seconds;
+  s->deltaTime = currentFrame - s->lastFrame;
+  s->lastFrame = currentFrame;
+  return RM_OK;
+}
+
+// processInput  main.cpp:155-195
+int rm_input_process(rm_input_state* s, uint32_t held, rm_camera_state* cam) {
+  if (!s || !cam) return RM_ERR_INVALID;
+  const bool W = held & RM_HELD_W, A = held & RM_HELD_A, S = held & RM_HELD_S,
+             D = held & RM_HELD_D;
+  if (held & RM_HELD_ESCAPE) s->shouldClose = 1;
+  s->zaxisNeg = W;
+  s->zaxisPos = S;
+  s->xaxisPos = D;
+  s->xaxisNeg = A;
+  // diagonal pairs only: W+S or A+D alone keep full speed (main.cpp:185-188)
+  const bool half = (W && A) || (W && D) || (A && S) || (S && D);
+  s->halfSpeed = half ? 1.0f : 0.0f;
+  return rm_camera_look_at(cam, s->zaxisNeg, s->zaxisPos, s->xaxisNeg, s->xaxisPos,
+                           s->halfSpeed != 0.0f, s->deltaTime);
+}
+
+// key_callback  main.cpp:197-217
+int rm_input_key(rm_input_state* s, int32_t key, int32_t action) {
+  if (!s) return RM_ERR_INVALID;
+  if (action != RM_PRESS) return RM_OK;
+  if (key == RM_KEY_UP && s->bounce < 5) s->bounce += 1;
+  if (key == RM_KEY_DOWN && s->bounce > 0) s->bounce -= 1;
+  if (key == RM_KEY_F1) s->AA = !s->AA;
+  if (key == RM_KEY_L) s->showQuad = !s->showQuad;  // glPolygonMode only: no render effect
+  return RM_OK;
+}
+
+// mouse_callback  main.cpp:219-234 + MouseInput::ProcessMouseOffset MousePosition.cpp:10-22
+int rm_input_mouse(rm_input_state* s, double xpos, double ypos, rm_camera_state* cam) {
+  if (!s || !cam) return RM_ERR_INVALID;
+  if (s->firstMouse) {
+    s->lastX = (float)xpos;
+    s->lastY = (float)ypos;
+    s->firstMouse = 0;
+  }
+  float xoffset = (float)((double)s->lastX - xpos);  // float - double is a double subtraction
+  float yoffset = (float)((double)s->lastY - ypos);
+  s->lastX = (float)xpos;
+  s->lastY = (float)ypos;
+  xoffset *= s->mouseSensitivity;
+  yoffset *= s->mouseSensitivity;
+  s->yaw += xoffset;
+  s->pitch += yoffset;
+  return rm_camera_set_mouse(cam, (float)-xpos, (float)-ypos);
+}
+
+// MouseInput::EulerAngles  MousePosition.cpp:24-33.  As written there: cos/sin of
+// the PRODUCT, and the unqualified cos/sin of a float resolve to the C library's
+// double functions (no std:: float overload is visible), so the trig runs in
+// double and each component is rounded to float on assignment.
+int rm_input_euler_angles(const rm_input_state* s, float out[3]) {
+  if (!s || !out) return RM_ERR_INVALID;
+  const double ry = radians(s->yaw), rp = radians(s->pitch);
+  vec3 front;
+  front.x = (float)std::cos(ry * std::cos(rp));
+  front.y = (float)std::sin(rp);
+  front.z = (float)std::sin(ry * std::cos(rp));
+  st3(out, normalize(front));
+  return RM_OK;
+}
+
+// main.cpp:101-120, the uploads input drives
+int rm_input_to_uniforms(const rm_input_state* s, const rm_camera_state* cam, rm_uniforms* u) {
+  if (!s || !cam || !u) return RM_ERR_INVALID;
+  rm_camera_to_uniform(cam, &u->camera);
+  u->iTime = s->lastFrame;
+  u->AA = s->AA ? 1 : 0;
+  u->bounceVar = s->bounce;
+  rm_input_euler_angles(s, u->mouse);
+  u->iMouse[0] = s->yaw;
+  u->iMouse[1] = s->pitch;
+  return RM_OK;
+}
+
 // Defaults: main.cpp:27,30 (AA on, bounce 0), light block main.cpp:108-114,
 // start-up camera main.cpp:40 after lookAt with zero mouse.
 int rm_default_uniforms(rm_uniforms* u) {

@@ -88,6 +88,22 @@ class rm_camera_state(C.Structure):
                 ("up", C.c_float * 3), ("right", C.c_float * 3)]
 
 
+class rm_input_state(C.Structure):
+    _fields_ = [("zaxisPos", C.c_int32), ("zaxisNeg", C.c_int32), ("xaxisPos", C.c_int32),
+                ("xaxisNeg", C.c_int32), ("AA", C.c_int32), ("showQuad", C.c_int32),
+                ("halfSpeed", C.c_float), ("bounce", C.c_int32), ("deltaTime", C.c_float),
+                ("lastFrame", C.c_float), ("lastX", C.c_float), ("lastY", C.c_float),
+                ("firstMouse", C.c_int32), ("pitch", C.c_float), ("yaw", C.c_float),
+                ("mouseSensitivity", C.c_float), ("shouldClose", C.c_int32)]
+
+
+# GLFW key / action codes (glfw3.h) and held-key bits, as in include/rm_api.h
+KEY_A, KEY_D, KEY_L, KEY_S, KEY_W = 65, 68, 76, 83, 87
+KEY_ESCAPE, KEY_DOWN, KEY_UP, KEY_F1 = 256, 264, 265, 290
+RELEASE, PRESS, REPEAT = 0, 1, 2
+HELD_W, HELD_A, HELD_S, HELD_D, HELD_ESCAPE = 1, 2, 4, 8, 16
+
+
 # ---- library loading --------------------------------------------------------------
 _lib: Optional[C.CDLL] = None
 
@@ -132,6 +148,16 @@ _SIGS = {
     "rm_camera_look_at": (C.c_int, [C.POINTER(rm_camera_state), C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_int, C.c_float]),
     "rm_camera_to_uniform": (C.c_int, [C.POINTER(rm_camera_state), C.POINTER(rm_camera)]),
+    "rm_input_init": (C.c_int, [C.POINTER(rm_input_state), C.c_int32, C.c_int32]),
+    "rm_input_begin_frame": (C.c_int, [C.POINTER(rm_input_state), C.c_double]),
+    "rm_input_process": (C.c_int, [C.POINTER(rm_input_state), C.c_uint32,
+                                   C.POINTER(rm_camera_state)]),
+    "rm_input_key": (C.c_int, [C.POINTER(rm_input_state), C.c_int32, C.c_int32]),
+    "rm_input_mouse": (C.c_int, [C.POINTER(rm_input_state), C.c_double, C.c_double,
+                                 C.POINTER(rm_camera_state)]),
+    "rm_input_euler_angles": (C.c_int, [C.POINTER(rm_input_state), C.POINTER(C.c_float)]),
+    "rm_input_to_uniforms": (C.c_int, [C.POINTER(rm_input_state), C.POINTER(rm_camera_state),
+                                       C.POINTER(rm_uniforms)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(rm_uniforms)]),
 }
@@ -224,6 +250,58 @@ class Camera:
 
     @property
     def state(self) -> rm_camera_state:
+        return self._s
+
+
+# ---- interactive input (main.cpp:20-39, 93-95, 155-234; MousePosition.cpp) -------------
+class Input:
+    """The reference's GLFW input globals and callbacks for one window.
+
+    Owns the ``Camera`` the callbacks move (main.cpp:40's arguments by default) and the
+    ``MouseInput`` angles.  A windowing front-end calls ``begin_frame(glfwGetTime())``,
+    ``processInput(held)`` once per frame and forwards its key / cursor events to
+    ``key_callback`` / ``mouse_callback``; ``to_uniforms`` then fills the per-frame uploads
+    of main.cpp:101-120.  Every rule (diagonal half speed, bounce 0..5, PRESS-only toggles,
+    first-mouse latch, float/double rounding) is librm's ``rm_input_*``.
+    """
+
+    def __init__(self, SCREEN_WIDTH: int = 1080, SCREEN_HEIGHT: int = 1080,
+                 camera: Optional[Camera] = None):
+        self._s = rm_input_state()
+        _check(lib().rm_input_init(C.byref(self._s), SCREEN_WIDTH, SCREEN_HEIGHT))
+        self.camera = camera if camera is not None else Camera(
+            SCREEN_WIDTH, SCREEN_HEIGHT, 0.025, 10.0, (0, 0, 0), (0, 0, -1), (0, 1, 0))
+
+    def begin_frame(self, now: float) -> None:  # main.cpp:93-95
+        _check(lib().rm_input_begin_frame(C.byref(self._s), now))
+
+    def processInput(self, held: int = 0) -> None:  # main.cpp:155-195
+        """``held``: OR of HELD_* for the keys glfwGetKey reports as pressed."""
+        _check(lib().rm_input_process(C.byref(self._s), held, C.byref(self.camera.state)))
+
+    def key_callback(self, key: int, scancode: int = 0, action: int = PRESS,
+                     mods: int = 0) -> None:  # main.cpp:197-217
+        _check(lib().rm_input_key(C.byref(self._s), key, action))
+
+    def mouse_callback(self, xpos: float, ypos: float) -> None:  # main.cpp:219-234
+        _check(lib().rm_input_mouse(C.byref(self._s), xpos, ypos, C.byref(self.camera.state)))
+
+    def EulerAngles(self) -> tuple:  # MousePosition.cpp:24-33
+        out = (C.c_float * 3)()
+        _check(lib().rm_input_euler_angles(C.byref(self._s), out))
+        return tuple(out)
+
+    def to_uniforms(self, u: Optional[rm_uniforms] = None) -> rm_uniforms:
+        u = default_uniforms() if u is None else u
+        _check(lib().rm_input_to_uniforms(C.byref(self._s), C.byref(self.camera.state),
+                                          C.byref(u)))
+        return u
+
+    def __getattr__(self, name):
+        return getattr(object.__getattribute__(self, "_s"), name)
+
+    @property
+    def state(self) -> rm_input_state:
         return self._s
 
 

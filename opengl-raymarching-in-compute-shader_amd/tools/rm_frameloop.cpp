@@ -5,9 +5,20 @@
 // (:136-143) and its runtime toggles as flags (bounce 0..5 :199-204, AA F1
 // :206-207).  Optionally dumps the last frame as a PPM (top row first).
 //
+// --input FILE replays a recorded input script through rm::Input (the
+// reference's processInput / key_callback / mouse_callback)
+// instead of the sweep; one line per event, in order:
+//   frame <now_seconds> <held>   begin a frame: clock, processInput(held), render
+//   key <glfw_key> <action>      key_callback
+//   mouse <xpos> <ypos>          mouse_callback
+// held = OR of W 1, A 2, S 4, D 8, ESC 16.  The loop stops after ESC, like
+// while (!glfwWindowShouldClose(window)) (main.cpp:92).
+//
 //   rm_frameloop [--width W] [--height H] [--frames N] [--bounces B] [--aa 0|1]
 //                [--hard-shadows] [--kernel auto|pixel|wavequeue] [--dump out.ppm]
+//                [--input script.txt]
 #include <rm/camera.hpp>
+#include <rm/input.hpp>
 #include <rm/texture.hpp>
 
 #include <chrono>
@@ -21,6 +32,7 @@ int main(int argc, char** argv) {
   int W = 1080, H = 1080, frames = 120, bounce = 0, aa = 1, shadow = RM_SHADOW_SOFT;
   int kernel = RM_KERNEL_AUTO;
   const char* dump = nullptr;
+  const char* script = nullptr;
   for (int i = 1; i < argc; ++i) {
     auto next = [&](const char* flag) -> const char* {
       if (i + 1 >= argc) {
@@ -36,6 +48,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--aa")) aa = std::atoi(next("--aa"));
     else if (!std::strcmp(argv[i], "--hard-shadows")) shadow = RM_SHADOW_HARD;
     else if (!std::strcmp(argv[i], "--dump")) dump = next("--dump");
+    else if (!std::strcmp(argv[i], "--input")) script = next("--input");
     else if (!std::strcmp(argv[i], "--kernel")) {
       std::string k = next("--kernel");
       kernel = k == "pixel" ? RM_KERNEL_PIXEL : k == "wavequeue" ? RM_KERNEL_WAVEQUEUE : RM_KERNEL_AUTO;
@@ -49,7 +62,21 @@ int main(int argc, char** argv) {
 
   // main.cpp:40 — the global camera; the sweep moves it to (0,0,15)
   rm::Camera camera(W, H, 0.025f, 10.0f, rm::vec3(0, 0, 0), rm::vec3(0, 0, -1), rm::vec3(0, 1, 0));
-  camera.cameraPos = rm::vec3(0.0f, 0.0f, 15.0f);
+  rm::Input input(camera, W, H);  // main.cpp:23-39 globals + callbacks
+  FILE* events = nullptr;
+  if (script) {
+    events = std::fopen(script, "r");
+    if (!events) {
+      std::fprintf(stderr, "cannot open %s\n", script);
+      return 2;
+    }
+    // the reference starts at bounce 0 / AA on; the flags seed the toggles
+    for (int b = 0; b < bounce; ++b) input.key_callback(RM_KEY_UP, 0, RM_PRESS, 0);
+    if (!aa) input.key_callback(RM_KEY_F1, 0, RM_PRESS, 0);
+    frames = 1 << 30;
+  } else {
+    camera.cameraPos = rm::vec3(0.0f, 0.0f, 15.0f);
+  }
   rm::Texture tex(W, H);  // main.cpp:70-71
   if (int rc = tex.GenerateTexture(RM_OUT_RGBA8, kernel); rc != RM_OK) {
     std::fprintf(stderr, "GenerateTexture failed (%d): %s\n", rc, rm_last_error(nullptr));
@@ -63,14 +90,46 @@ int main(int argc, char** argv) {
   double lastTime = 0.0;
   unsigned counter = 0, total = 0;
   for (int f = 0; f < frames; ++f) {
-    // synthetic input instead of processInput/mouse_callback (SURVEY 8(d) sweep)
-    const double yaw = frames > 1 ? -20.0 + 40.0 * f / (frames - 1) : 0.0;
-    camera.setMouse((float)(yaw / 0.025), (float)(-5.0 / 0.025));
-    camera.lookAt(false, false, false, false, false, 0.0f);
+    float iTime = (float)f / 60.0f;
+    if (events) {  // recorded input: apply events up to and including the next frame line
+      if (input.shouldClose()) break;
+      char kind[16];
+      bool frame_line = false;
+      while (!frame_line && std::fscanf(events, "%15s", kind) == 1) {
+        double a = 0.0, b = 0.0;
+        if (std::fscanf(events, "%lf %lf", &a, &b) != 2) {
+          std::fprintf(stderr, "bad input line after '%s'\n", kind);
+          return 2;
+        }
+        if (!std::strcmp(kind, "frame")) {
+          input.beginFrame(a);
+          input.processInput((unsigned)b);
+          frame_line = true;
+        } else if (!std::strcmp(kind, "key")) {
+          input.key_callback((int)a, 0, (int)b, 0);
+        } else if (!std::strcmp(kind, "mouse")) {
+          input.mouse_callback(a, b);
+        } else {
+          std::fprintf(stderr, "unknown input event '%s'\n", kind);
+          return 2;
+        }
+      }
+      if (!frame_line) break;  // script exhausted
+      rm_uniforms u{};
+      input.toUniforms(&u);
+      iTime = u.iTime;
+      aa = input.AA();
+      bounce = input.bounce();
+    } else {
+      // synthetic input instead of processInput/mouse_callback (SURVEY 8(d) sweep)
+      const double yaw = frames > 1 ? -20.0 + 40.0 * f / (frames - 1) : 0.0;
+      camera.setMouse((float)(yaw / 0.025), (float)(-5.0 / 0.025));
+      camera.lookAt(false, false, false, false, false, 0.0f);
+    }
     const rm_camera cu = camera.toUniform();
 
     rm::useShader(marching);  // main.cpp:99-120
-    rm::setFloat(marching, "iTime", (float)f / 60.0f);
+    rm::setFloat(marching, "iTime", iTime);
     rm::setuInt(marching, "workgroups", &workgroups);
     rm::setVec4(marching, "camera.pos", cu.pos[0], cu.pos[1], cu.pos[2], 0.0f);
     rm::setVec4(marching, "camera.dir", cu.dir[0], cu.dir[1], cu.dir[2], 0.0f);
@@ -85,6 +144,10 @@ int main(int argc, char** argv) {
     rm::setFloat(marching, "light.quadratic", 0.00032f);
     rm::setBool(marching, "AA", aa != 0);
     rm::setInt(marching, "bounceVar", bounce);
+    rm_uniforms mu{};  // main.cpp:118-119 (accepted, unused by the shader)
+    input.toUniforms(&mu);
+    rm::setVec3(marching, "mouse", mu.mouse[0], mu.mouse[1], mu.mouse[2]);
+    rm::setVec2(marching, "iMouse", mu.iMouse[0], mu.iMouse[1]);
     rm::setInt(marching, "shadow_mode", shadow);
 
     if (rm::dispatchCompute(marching) != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
