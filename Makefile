@@ -22,7 +22,7 @@ LIBRM    := $(PKG)/librm.so
 ORACLE   := oracle/_build/librm_oracle.so
 DRIVER   := $(PKG)/rm_frameloop
 
-RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_host.cpp
+RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_table.hip $(CSRC)/rm_host.cpp
 RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp include/rm_api.h
 
 .PHONY: all librm oracle driver goldens clean
@@ -39,7 +39,7 @@ $(PKG)/build/rm_host.o: $(CSRC)/rm_host.cpp $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 
-$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_host.o
+$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_table.o $(PKG)/build/rm_host.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h

@@ -181,6 +181,52 @@ int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
 int rm_graph_enable(rm_ctx *ctx, int enable);
 int rm_graph_dispatch(rm_ctx *ctx);
 
+/* ---- runtime scene table ------------------------------
+ * The reference's scene is the hard-coded sdf() of computeShader.glsl:107-123:
+ * an opU chain of primitives, each a RayHit {distance, colour, id, material}.
+ * rm_set_scene replaces it with a table of up to RM_MAX_PRIMITIVES such
+ * entries, evaluated in table order with the same opU rule (a later entry wins
+ * unless the running distance is strictly smaller, glsl:105).  The table is
+ * staged in LDS by every workgroup of the table kernel.  rm_default_scene
+ * returns the reference's scene as a table; rendered through the table kernel
+ * it gives the same image as the built-in scene's specialised kernel.
+ * The shading rules stay the reference's: id 7 takes the floor branch
+ * (shadow, no bounce; glsl:240-247, 177) and material 0 (MATTE) stops the
+ * bounce colour accumulation (glsl:189-190). */
+#define RM_MAX_PRIMITIVES 32
+#define RM_PRIM_SPHERE 0  /* sdSphere(q, r)                               glsl:83 */
+#define RM_PRIM_BOX 1     /* sdBox(q, b)                                  glsl:87-91 */
+#define RM_PRIM_BLEND 2   /* mix(sdBox(q, b), sdSphere(q, r), sin(iTime)/2 + 0.5)  glsl:115-117 */
+#define RM_PRIM_TORUS 3   /* sdTorus(q, (R, r))                           glsl:93-96 */
+#define RM_PRIM_CAPSULE 4 /* sdCapsule(q, a, b, r)                        glsl:98-103 */
+#define RM_PRIM_PLANE 5   /* sdPlane(q, (nx, ny, nz, w))                  glsl:85 */
+#define RM_SWIZZLE_XYZ 0  /* q = p - center */
+#define RM_SWIZZLE_XZY 1  /* q = (p - center).xzy  (the torus of glsl:119) */
+#define RM_PAINT_SOLID 0    /* RayHit.color = color */
+#define RM_PAINT_CHECKERS 1 /* RayHit.color = checkers(p)                 glsl:77-80 */
+
+typedef struct rm_primitive {
+  int32_t type;    /* RM_PRIM_* */
+  int32_t swizzle; /* RM_SWIZZLE_* */
+  int32_t id;      /* RayHit.id (glsl:42) */
+  int32_t paint;   /* RM_PAINT_* */
+  float material;  /* RayHit.material: 1 REFLECTIVE, 0 MATTE (glsl:4-5) */
+  float color[3];
+  float center[3];
+  /* sphere {r}; box {bx, by, bz}; blend {bx, by, bz, r}; torus {R, r};
+   * capsule {ax, ay, az, bx, by, bz, r}; plane {nx, ny, nz, w} */
+  float param[7];
+} rm_primitive;
+
+/* The reference scene (glsl:107-123) as 6 table entries (the blended box and
+ * sphere of glsl:115-117 are one RM_PRIM_BLEND entry, id 4).  *n = 6. */
+int rm_default_scene(rm_primitive *out, int32_t capacity, int32_t *n);
+/* Render with `prims[0..n)` from the next dispatch on.  prims == NULL and
+ * n == 0 return to the built-in scene (the specialised kernel). */
+int rm_set_scene(rm_ctx *ctx, const rm_primitive *prims, int32_t n);
+/* The table in use (*n = 0: the built-in scene). */
+int rm_get_scene(const rm_ctx *ctx, rm_primitive *out, int32_t capacity, int32_t *n);
+
 /* ---- device-side interop (plain pointers; for stream/collective plumbing) - */
 /* Use an external stream (hipStream_t passed as void*); NULL = own stream. */
 int rm_set_stream(rm_ctx *ctx, void *hip_stream);

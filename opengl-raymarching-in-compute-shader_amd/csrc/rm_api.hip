@@ -21,6 +21,7 @@ namespace rm {
 extern int g_wq_batch;
 extern int g_wq_blocks_per_cu;
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s);
@@ -51,6 +52,10 @@ struct rm_ctx {
   uint32_t* d_queue = nullptr;
   float* d_prep = nullptr;        // k_prep's per-frame step-0 values (rm_scene.hpp PrepSlot)
   float* d_uv = nullptr;          // per-column / per-row uv table (Frame::uvx / uvy)
+  uint32_t* d_scene = nullptr;    // runtime scene table (rm_set_scene), compiled words
+  int nprims = 0;                 // 0: the built-in scene and its specialised kernel
+  std::vector<rm_primitive> scene;     // the table as given (rm_get_scene)
+  std::vector<uint32_t> scene_words;   // host copy of d_scene (source of the async upload)
   bool dispatched = false;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -59,6 +64,7 @@ struct rm_ctx {
   int64_t launches = 0;
   bool graph_on = false;
   int graph_aa = -1;  // AA value the graphs were captured for (grid shape depends on it)
+  int graph_table = -1;  // whether the graph holds the table kernel (1) or the built-in one (0)
   rm_graph_slot gs;
   std::string err;
 };
@@ -127,6 +133,8 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
   F.queue = c->d_queue;
   F.prep = c->d_prep;
+  F.scene = c->nprims ? reinterpret_cast<const float*>(c->d_scene) : nullptr;
+  F.nprims = c->nprims;
   return F;
 }
 
@@ -137,6 +145,7 @@ void graph_release(rm_ctx* c) {
   if (g.graph) (void)hipGraphDestroy(g.graph);
   g = rm_graph_slot();
   c->graph_aa = -1;
+  c->graph_table = -1;
 }
 
 void free_all(rm_ctx* c) {
@@ -148,6 +157,7 @@ void free_all(rm_ctx* c) {
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->d_prep) (void)hipFree(c->d_prep);
   if (c->d_uv) (void)hipFree(c->d_uv);
+  if (c->d_scene) (void)hipFree(c->d_scene);
   for (auto& p : c->ev_pool) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
@@ -161,6 +171,7 @@ void free_all(rm_ctx* c) {
   c->d_queue = nullptr;
   c->d_prep = nullptr;
   c->d_uv = nullptr;
+  c->d_scene = nullptr;
   c->stream = nullptr;
 }
 
@@ -386,7 +397,9 @@ int rm_dispatch(rm_ctx* c) {
     RM_HIP(c, hipMemsetAsync(c->d_queue, 0, 256, c->stream));
   }
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
-  hipError_t e = (kernel == RM_KERNEL_PIXEL)
+  // a runtime scene table renders with the table kernel whatever the variant
+  hipError_t e = c->nprims ? rm::launch_table(F, c->cfg.counters != 0, c->stream)
+                 : (kernel == RM_KERNEL_PIXEL)
                      ? rm::launch_pixel(F, c->cfg.counters != 0, c->stream)
                      : rm::launch_wavequeue(F, c->cfg.counters != 0, c->stream, c->num_cus);
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
@@ -503,7 +516,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   int rc = RM_OK;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess) {
-    const hipError_t e1 = rm::launch_pixel(F, false, cs);
+    const hipError_t e1 = F.nprims ? rm::launch_table(F, false, cs) : rm::launch_pixel(F, false, cs);
     e = hipStreamEndCapture(cs, &g.graph);
     if (e == hipSuccess) e = e1;
   }
@@ -519,6 +532,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
     return rc;
   }
   c->graph_aa = F.aa;
+  c->graph_table = F.nprims ? 1 : 0;
   return RM_OK;
 }
 
@@ -544,7 +558,9 @@ int rm_graph_dispatch(rm_ctx* c) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   rmd::Frame F = make_frame(c);
-  if (F.aa != c->graph_aa && (rc = graph_capture(c, F)) != RM_OK) return rc;
+  if ((F.aa != c->graph_aa || (F.nprims ? 1 : 0) != c->graph_table) &&
+      (rc = graph_capture(c, F)) != RM_OK)
+    return rc;
   rm_graph_slot& g = c->gs;
   void* args[] = {&F};
   for (size_t k = 0; k < g.nodes; ++k) {
@@ -570,6 +586,44 @@ int rm_graph_dispatch(rm_ctx* c) {
   RM_HIP(c, hipGraphLaunch(g.exec, c->stream));
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
   c->dispatched = true;
+  return RM_OK;
+}
+
+// ---- runtime scene table ----------------------------------------------------------
+int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
+  if (!c) return RM_ERR_INVALID;
+  if (!prims && n == 0) {  // back to the built-in scene
+    c->nprims = 0;
+    c->scene.clear();
+    return RM_OK;
+  }
+  std::vector<uint32_t> words((size_t)(n > 0 ? n : 0) * rm::TABLE_WORDS);
+  const char* why = "rm_set_scene: bad table";
+  if (rm::compile_scene(prims, n, words.data(), &why) != RM_OK) return fail(c, RM_ERR_INVALID, why);
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if (!c->d_scene) {
+    RM_HIP(c, hipMalloc(&c->d_scene, (size_t)RM_MAX_PRIMITIVES * rm::TABLE_WORDS * sizeof(uint32_t)));
+  }
+  // Ordered on the context's stream after the frames already queued (they keep
+  // reading the previous table); the host copy must outlive the async copy, so
+  // wait for it before the staging vector is replaced.
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  c->scene_words = std::move(words);
+  RM_HIP(c, hipMemcpyAsync(c->d_scene, c->scene_words.data(), c->scene_words.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, c->stream));
+  c->scene.assign(prims, prims + n);
+  c->nprims = n;
+  return RM_OK;
+}
+
+int rm_get_scene(const rm_ctx* c, rm_primitive* out, int32_t capacity, int32_t* n) {
+  if (!c || !n) return RM_ERR_INVALID;
+  *n = c->nprims;
+  if (out && c->nprims) {
+    if (capacity < c->nprims) return RM_ERR_INVALID;
+    std::memcpy(out, c->scene.data(), sizeof(rm_primitive) * c->nprims);
+  }
   return RM_OK;
 }
 

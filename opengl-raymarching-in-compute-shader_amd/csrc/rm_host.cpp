@@ -8,8 +8,10 @@
 //     main.cpp:99-120);
 //   * synthetic sweep frames and the row-shard map.
 // Compiled with -ffp-contract=off: every float op is one IEEE binary32 op.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 
 #include "rm_internal.hpp"
 
@@ -369,6 +371,97 @@ int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, in
 }
 
 }  // extern "C"
+
+// ---- runtime scene table ----------------------------------
+namespace {
+rm_primitive prim(int32_t type, int32_t swz, int32_t id, int32_t paint, float material,
+                  std::initializer_list<float> color, std::initializer_list<float> center,
+                  std::initializer_list<float> param) {
+  rm_primitive p;
+  std::memset(&p, 0, sizeof p);
+  p.type = type;
+  p.swizzle = swz;
+  p.id = id;
+  p.paint = paint;
+  p.material = material;
+  std::copy(color.begin(), color.end(), p.color);
+  std::copy(center.begin(), center.end(), p.center);
+  std::copy(param.begin(), param.end(), p.param);
+  return p;
+}
+}  // namespace
+
+extern "C" int rm_default_scene(rm_primitive* out, int32_t capacity, int32_t* n) {
+  if (!n) return RM_ERR_INVALID;
+  // computeShader.glsl:107-123, in opU order
+  const rm_primitive scene[6] = {
+      prim(RM_PRIM_SPHERE, RM_SWIZZLE_XYZ, 0, RM_PAINT_SOLID, 1.0f, {0.1804f, 0.6f, 0.2157f},
+           {15.0f, 0.0f, -10.0f}, {3.0f}),                                         // :111
+      prim(RM_PRIM_SPHERE, RM_SWIZZLE_XYZ, 1, RM_PAINT_SOLID, 1.0f, {0.0f, 0.851f, 1.0f},
+           {-25.0f, 0.0f, -10.0f}, {3.0f}),                                        // :112
+      prim(RM_PRIM_BLEND, RM_SWIZZLE_XYZ, 4, RM_PAINT_SOLID, 1.0f, {0.4863f, 0.3529f, 0.702f},
+           {-5.0f, 0.0f, -10.0f}, {3.0f, 2.5f, 2.5f, 3.0f}),                       // :115-117
+      prim(RM_PRIM_TORUS, RM_SWIZZLE_XZY, 5, RM_PAINT_SOLID, 1.0f, {0.9137f, 0.549f, 0.0f},
+           {-5.0f, 0.0f, 10.0f}, {2.5f, 0.5f}),                                    // :119
+      prim(RM_PRIM_CAPSULE, RM_SWIZZLE_XYZ, 6, RM_PAINT_SOLID, 1.0f, {0.8f, 0.0902f, 0.4824f},
+           {-5.0f, -2.0f, -30.0f}, {-0.1f, 0.1f, -0.1f, 2.0f, 4.0f, 2.0f, 1.0f}),  // :120
+      prim(RM_PRIM_PLANE, RM_SWIZZLE_XYZ, 7, RM_PAINT_CHECKERS, 0.0f, {0.0f, 0.0f, 0.0f},
+           {0.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f, 5.5f}),                          // :121
+  };
+  *n = 6;
+  if (out) {
+    if (capacity < 6) return RM_ERR_INVALID;
+    std::memcpy(out, scene, sizeof scene);
+  }
+  return RM_OK;
+}
+
+namespace rm {
+
+int compile_scene(const rm_primitive* prims, int32_t n, uint32_t* out, const char** why) {
+  auto bad = [&](const char* m) {
+    if (why) *why = m;
+    return RM_ERR_INVALID;
+  };
+  if (!prims || n < 1 || n > RM_MAX_PRIMITIVES)
+    return bad("rm_set_scene: need 1..RM_MAX_PRIMITIVES primitives");
+  for (int32_t k = 0; k < n; ++k) {
+    const rm_primitive& p = prims[k];
+    if (p.type < RM_PRIM_SPHERE || p.type > RM_PRIM_PLANE) return bad("rm_set_scene: unknown primitive type");
+    if (p.swizzle != RM_SWIZZLE_XYZ && p.swizzle != RM_SWIZZLE_XZY) return bad("rm_set_scene: unknown swizzle");
+    if (p.paint != RM_PAINT_SOLID && p.paint != RM_PAINT_CHECKERS) return bad("rm_set_scene: unknown paint");
+    uint32_t* w = out + (size_t)k * TABLE_WORDS;
+    float f[TABLE_WORDS];
+    std::memset(f, 0, sizeof f);
+    f[TW_MATERIAL] = p.material;
+    for (int j = 0; j < 3; ++j) {
+      f[TW_COLOR + j] = p.color[j];
+      f[TW_CENTER + j] = p.center[j];
+    }
+    float* q = f + TW_P;
+    const float* a = p.param;
+    switch (p.type) {
+      case RM_PRIM_CAPSULE: {  // glsl:100-101: ba = b - a, dot(ba, ba) = (x*x + y*y) + z*z
+        const float bax = a[3] - a[0], bay = a[4] - a[1], baz = a[5] - a[2];
+        q[0] = a[0], q[1] = a[1], q[2] = a[2];
+        q[3] = bax, q[4] = bay, q[5] = baz;
+        q[6] = (bax * bax + bay * bay) + baz * baz;
+        q[7] = a[6];
+        break;
+      }
+      default:
+        for (int j = 0; j < 7; ++j) q[j] = a[j];
+    }
+    std::memcpy(w, f, sizeof f);
+    w[TW_TYPE] = (uint32_t)p.type;
+    w[TW_SWIZZLE] = (uint32_t)p.swizzle;
+    w[TW_ID] = (uint32_t)p.id;
+    w[TW_PAINT] = (uint32_t)p.paint;
+  }
+  return RM_OK;
+}
+
+}  // namespace rm
 
 // ---- uniform lookup by GLSL name (shader.hpp:19-69 semantics) -----------------
 namespace rm {

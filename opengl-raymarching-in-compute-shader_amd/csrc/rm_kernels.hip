@@ -339,38 +339,7 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   return gamma(color);
 }
 
-// Dispatch order of the tile rows (RM_ROW_ORDER): 0 natural (bottom up),
-// 1 top down, 2 inside out (middle row first, then alternately below and above).
-// The slowest waves (rays grazing the floor near the horizon, silhouettes) sit
-// in the middle band of an upright view; started first they no longer form a
-// tail behind the cheap sky and near-floor rows (cfg3 1.24 -> 1.18 ms).
-#ifndef RM_ROW_ORDER
-#define RM_ROW_ORDER 2
-#endif
-__device__ __forceinline__ int tile_row(int b, int n) {
-  if (RM_ROW_ORDER == 1) return n - 1 - b;
-  if (RM_ROW_ORDER == 2) {
-    // mid, mid-1, mid+1, mid-2, ...: b < n covers [mid - n/2, mid + (n-1)/2] = [0, n-1]
-    const int mid = n / 2, k = (b + 1) >> 1;
-    return (b & 1) ? mid - k : mid + k;
-  }
-  return b;
-}
-
-// XCD-aware tile column: one-wave workgroups go round-robin to the 8 XCDs
-// (block b -> XCD b % 8), so consecutive blocks land in different L2s and the
-// 16-32 B row segments that neighbouring tiles store into one 128 B line are
-// written back separately (PMC: 2x write amplification).  Within each window of
-// 8 G blocks, XCD k takes the G adjacent tiles [k G, (k+1) G): a line's
-// segments meet in one L2, while the XCDs still interleave at G-tile grain
-// (a coarse split, XCD k = columns [k gx/8, ...), unbalanced the XCDs: 2x slower).
-__device__ __forceinline__ int tile_col(int b, int gx, int G) {
-  const int win = 8 * G;
-  const int w0 = (b / win) * win;
-  if (w0 + win > gx) return b;  // ragged last window: natural order
-  const int r = b - w0;
-  return w0 + (r & 7) * G + (r >> 3);
-}
+// tile_row / tile_col (dispatch order): rm_scene.hpp
 
 // main glsl:291-344, one thread per pixel.  A 256-thread workgroup covers a
 // 16x16 pixel tile and each wave an 8x8 sub-tile, so the 64 rays of a wave

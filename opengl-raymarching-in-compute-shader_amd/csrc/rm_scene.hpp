@@ -81,6 +81,8 @@ struct Frame {
   unsigned long long* counters;  // 6 x u64 (counter builds)
   uint32_t* queue;       // work-queue head (wave-queue kernel), zeroed per dispatch
   const float* prep;     // step 0 of the primary rays (PrepSlot), written by k_prep
+  const float* scene;    // runtime scene table (rm_set_scene), TABLE_WORDS per primitive, or null
+  int32_t nprims;        // entries in `scene`
 };
 
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
@@ -700,6 +702,39 @@ __device__ __forceinline__ void cast_ray(const Frame& F, float uvx, float uvy, f
 __device__ __forceinline__ uint32_t quantize(float c) {
   float v = (c > 0.0f) ? ((c < 1.0f) ? c : 1.0f) : 0.0f;
   return (uint32_t)(v * 255.0f + 0.5f);
+}
+
+// Dispatch order of the tile rows (RM_ROW_ORDER): 0 natural (bottom up),
+// 1 top down, 2 inside out (middle row first, then alternately below and above).
+// The slowest waves (rays grazing the floor near the horizon, silhouettes) sit
+// in the middle band of an upright view; started first they no longer form a
+// tail behind the cheap sky and near-floor rows (cfg3 1.24 -> 1.18 ms).
+#ifndef RM_ROW_ORDER
+#define RM_ROW_ORDER 2
+#endif
+__device__ __forceinline__ int tile_row(int b, int n) {
+  if (RM_ROW_ORDER == 1) return n - 1 - b;
+  if (RM_ROW_ORDER == 2) {
+    // mid, mid-1, mid+1, mid-2, ...: b < n covers [mid - n/2, mid + (n-1)/2] = [0, n-1]
+    const int mid = n / 2, k = (b + 1) >> 1;
+    return (b & 1) ? mid - k : mid + k;
+  }
+  return b;
+}
+
+// XCD-aware tile column: one-wave workgroups go round-robin to the 8 XCDs
+// (block b -> XCD b % 8), so consecutive blocks land in different L2s and the
+// 16-32 B row segments that neighbouring tiles store into one 128 B line are
+// written back separately (PMC: 2x write amplification).  Within each window of
+// 8 G blocks, XCD k takes the G adjacent tiles [k G, (k+1) G): a line's
+// segments meet in one L2, while the XCDs still interleave at G-tile grain
+// (a coarse split, XCD k = columns [k gx/8, ...), unbalanced the XCDs: 2x slower).
+__device__ __forceinline__ int tile_col(int b, int gx, int G) {
+  const int win = 8 * G;
+  const int w0 = (b / win) * win;
+  if (w0 + win > gx) return b;  // ragged last window: natural order
+  const int r = b - w0;
+  return w0 + (r & 7) * G + (r >> 3);
 }
 
 // Global row of a launch-local row (row sharding).

@@ -1,0 +1,338 @@
+// rm_table.hip — the runtime-scene-table path.
+//
+// The reference hard-codes its scene in sdf() (computeShader.glsl:107-123).
+// This kernel renders any scene given as a table of primitives (rm_set_scene,
+// include/rm_api.h), with the reference's march / normal / shadow / light /
+// bounce logic (glsl:125-344) unchanged around a generic sdf:
+//
+//   * each workgroup stages the table (n x 80 B) from HBM into LDS once; every
+//     sdf() step then loops over the LDS entries in table order.  All lanes
+//     read the same entry (an LDS broadcast, no bank conflicts) and the
+//     primitive type is made wave-uniform (readfirstlane), so the per-type
+//     switch is a scalar branch;
+//   * opU (glsl:105) as in the GLSL: a later entry wins unless the running
+//     distance is strictly smaller; the hit's colour / id / material are read
+//     from the winning entry after the march (the colour at the same point);
+//   * every float operation is the IEEE one the GLSL specifies:
+//     correctly rounded sqrt and division throughout, no contraction — the
+//     specialised kernel's exactness arguments (bounded culling, linear exits,
+//     proven-exact sqrt / reciprocal sequences over bounded domains) depend on
+//     the built-in scene's geometry and are not used here.
+//
+// For the reference scene (rm_default_scene) the image equals the built-in
+// kernel's bit for bit (tests/test_gpu_scene.py); other tables are checked
+// against the oracle's table mode (oracle/rm_oracle.c rmo_render_scene).
+#include <hip/hip_runtime.h>
+
+#include "rm_internal.hpp"
+#include "rm_scene.hpp"
+
+#ifndef RM_TABLE_LDS
+#define RM_TABLE_LDS 1  // 0: read the table through the scalar cache instead of LDS
+#endif
+
+namespace rmd {
+
+struct TCnt {
+  uint32_t rays, march, reflect, shadow, normals, lights;
+};
+
+using rm::TABLE_WORDS;
+
+__device__ __forceinline__ float isqrt_ieee(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float tlen(f3 a) { return isqrt_ieee(dot(a, a)); }
+// GLSL normalize over the full float range (v * (1 / sqrt(dot)))
+__device__ __forceinline__ f3 tnormalize(f3 a) { return muls(a, 1.0f / isqrt_ieee(dot(a, a))); }
+
+// One table entry's distance at p (glsl:83-103, 115-121).
+__device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float blend,
+                                           float omblend) {
+  f3 q = sub(p, mk(P[rm::TW_CENTER], P[rm::TW_CENTER + 1], P[rm::TW_CENTER + 2]));
+  if (__float_as_int(P[rm::TW_SWIZZLE]) == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
+  const float* a = P + rm::TW_P;
+  switch (type) {
+    case RM_PRIM_SPHERE:
+      return tlen(q) - a[0];
+    case RM_PRIM_BOX:
+    case RM_PRIM_BLEND: {
+      const f3 d = mk(fabsf(q.x) - a[0], fabsf(q.y) - a[1], fabsf(q.z) - a[2]);
+      const f3 m = mk(gmax(d.x, 0.0f), gmax(d.y, 0.0f), gmax(d.z, 0.0f));
+      const float box = gmin(gmax(d.x, gmax(d.y, d.z)), 0.0f) + tlen(m);
+      if (type == RM_PRIM_BOX) return box;
+      const float sph = tlen(q) - a[3];
+      return box * omblend + sph * blend;  // mix(box, sphere, blend)
+    }
+    case RM_PRIM_TORUS: {
+      const float l = isqrt_ieee(q.x * q.x + q.z * q.z) - a[0];
+      return isqrt_ieee(l * l + q.y * q.y) - a[1];
+    }
+    case RM_PRIM_CAPSULE: {
+      const f3 pa = sub(q, mk(a[0], a[1], a[2])), ba = mk(a[3], a[4], a[5]);
+      const float h = gmin(gmax(dot(pa, ba) / a[6], 0.0f), 1.0f);
+      return tlen(sub(pa, muls(ba, h))) - a[7];
+    }
+    default:  // RM_PRIM_PLANE
+      return dot(q, mk(a[0], a[1], a[2])) + a[3];
+  }
+}
+
+struct Table {
+  const float* t;  // LDS (or global) copy of the compiled table
+  int n;
+  float blend, omblend;
+
+  __device__ __forceinline__ const float* entry(int k) const { return t + k * TABLE_WORDS; }
+  __device__ __forceinline__ int type(int k) const {
+    return __builtin_amdgcn_readfirstlane(__float_as_int(entry(k)[rm::TW_TYPE]));
+  }
+  // sdf(p).hitpoint and the index of the opU winner
+  __device__ __forceinline__ float dist(f3 p, int& best) const {
+    float d = prim_dist(entry(0), type(0), p, blend, omblend);
+    best = 0;
+    for (int k = 1; k < n; ++k) {
+      const float dk = prim_dist(entry(k), type(k), p, blend, omblend);
+      const bool keep = d < dk;  // opU(t, new) = (t < new) ? t : new
+      best = keep ? best : k;
+      d = keep ? d : dk;
+    }
+    return d;
+  }
+  __device__ __forceinline__ f3 color(int k, f3 p) const {
+    const float* P = entry(k);
+    if (__float_as_int(P[rm::TW_PAINT]) == RM_PAINT_CHECKERS) {
+      const float c = checkers(p);
+      return mk(c, c, c);
+    }
+    return mk(P[rm::TW_COLOR], P[rm::TW_COLOR + 1], P[rm::TW_COLOR + 2]);
+  }
+  __device__ __forceinline__ int id(int k) const { return __float_as_int(entry(k)[rm::TW_ID]); }
+  __device__ __forceinline__ float material(int k) const { return entry(k)[rm::TW_MATERIAL]; }
+};
+
+struct THit {
+  float t;  // -1: the dummy RayHit {-1, 0, -1, 1.0} (glsl:128)
+  int id;
+  float material;
+  f3 color;
+};
+
+// RayMarch glsl:125-142 / reflectedRay glsl:144-161
+template <bool COUNT>
+__device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
+  const float tmax = reflected ? 200.0f : 400.0f;
+  const int nmax = reflected ? 256 : 512;
+  float t = 0.0f;
+  for (int i = 0; i < nmax; ++i) {
+    const f3 p = add(ro, muls(rd, t));
+    int k;
+    const float d = S.dist(p, k);
+    if (COUNT) {
+      if (reflected) c.reflect++;
+      else c.march++;
+    }
+    if (d < 0.000001f * t) return THit{t, S.id(k), S.material(k), S.color(k, p)};
+    if (d > tmax) break;
+    t += d;
+  }
+  return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+}
+
+// GetNormal glsl:278-288
+template <bool COUNT>
+__device__ f3 tnormal(const Table& S, f3 pos, TCnt& c) {
+  if (COUNT) c.normals++;
+  int k;
+  const float c0 = S.dist(pos, k);
+  const float x = S.dist(add(pos, mk(0.001f, 0.0f, 0.0f)), k);
+  const float y = S.dist(add(pos, mk(0.0f, 0.001f, 0.0f)), k);
+  const float z = S.dist(add(pos, mk(0.0f, 0.0f, 0.001f)), k);
+  return tnormalize(subs(mk(x, y, z), c0));
+}
+
+// softshadow glsl:201-216
+template <bool COUNT>
+__device__ float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
+  float res = 1.0f, t = 0.0f;
+  for (int i = 0; i < 16; ++i) {
+    int k;
+    const float h = S.dist(add(ro, muls(rd, t)), k);
+    if (COUNT) c.shadow++;
+    if (h < 0.001f) return 0.05f;
+    res = gmin(res, F.k * h / t);
+    t += h;
+  }
+  return res;
+}
+
+// bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
+// the colour unchanged (glsl:181, 189-190): the loop stops there.
+template <bool COUNT>
+__device__ f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 normal, f3 color,
+                      const THit& primary, TCnt& c) {
+  float prevMat = primary.material;
+  f3 prevColor = primary.color;
+  const f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
+  for (int i = 1; i <= F.bounces; ++i) {
+    if (prevMat == 0.0f) break;
+    rayDir = reflect(rayDir, normal);
+    THit h = tmarch<COUNT>(S, add(pos, muls(normal, 0.001f)), rayDir, true, c);
+    pos = add(pos, muls(rayDir, h.t));
+    // the normal of a miss on the last bounce is never read
+    if (h.t != -1.0f || i < F.bounces) normal = tnormal<COUNT>(S, pos, c);
+    if (h.t == -1.0f) {
+      h.color = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
+    } else {
+      if (COUNT) c.lights++;
+      h.color = point_light(F, h.color, normal, pos);
+    }
+    if (h.id == 7 && i < 3) {  // prevObject.material != MATTE here
+      const float sh = tshadow<COUNT>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      color = muls(color, sh / (float)i);
+    }
+    color = add(color, divs(mul(h.color, prevColor), (float)i));
+    prevColor = h.color;
+    prevMat = h.material;
+  }
+  return color;
+}
+
+// render glsl:218-251
+template <bool COUNT>
+__device__ f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
+  f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
+  const THit h = tmarch<COUNT>(S, ro, rd, false, c);
+  if (h.t != -1.0f) {
+    const f3 pos = add(ro, muls(rd, h.t));
+    const f3 normal = tnormal<COUNT>(S, pos, c);
+    if (COUNT) c.lights++;
+    color = point_light(F, h.color, normal, pos);
+    if (h.id == 7) {
+      const f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
+      const float sh = tshadow<COUNT>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      return gamma(muls(color, sh));
+    }
+    if (F.bounces > 0) color = tbounce<COUNT>(F, S, rd, pos, normal, color, h, c);
+  }
+  return gamma(color);
+}
+
+// Stage the table into LDS (one-wave workgroups: the barrier is cheap).
+__device__ __forceinline__ Table stage(const Frame& F, float* lds) {
+  Table S;
+  S.n = F.nprims;
+  S.blend = F.blend;
+  S.omblend = F.omblend;
+  if (RM_TABLE_LDS) {
+    for (int i = threadIdx.x; i < F.nprims * TABLE_WORDS; i += blockDim.x) lds[i] = F.scene[i];
+    __syncthreads();
+    S.t = lds;
+  } else {
+    S.t = F.scene;
+  }
+  return S;
+}
+
+__device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
+  atomicAdd(&F.counters[0], (unsigned long long)c.rays);
+  atomicAdd(&F.counters[1], (unsigned long long)c.march);
+  atomicAdd(&F.counters[2], (unsigned long long)c.reflect);
+  atomicAdd(&F.counters[3], (unsigned long long)c.shadow);
+  atomicAdd(&F.counters[4], (unsigned long long)c.normals);
+  atomicAdd(&F.counters[5], (unsigned long long)c.lights);
+}
+
+// main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
+template <bool COUNT>
+__global__ __launch_bounds__(64) void k_table_pixel(Frame F) {
+  extern __shared__ float lds[];
+  const Table S = stage(F, lds);
+  const int lane = threadIdx.x;
+  const int by = tile_row(blockIdx.y, gridDim.y);
+  const int bx = tile_col(blockIdx.x, gridDim.x, 4);
+  const int px = bx * 8 + (lane & 7);
+  const int lrow = by * 8 + (lane >> 3);
+  if (px >= F.width || lrow >= F.rows) return;
+  const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
+  const int py = global_row(F, lrow);
+  TCnt c = {0, 0, 0, 0, 0, 0};
+  if (py < 0) {
+    store_pixel(F, idx, 0.0f, 0.0f, 0.0f, 0.0f);
+    return;
+  }
+  f3 ro, rd;
+  cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
+  if (COUNT) c.rays++;
+  const f3 col = trender<COUNT>(F, S, ro, rd, c);
+  store_pixel(F, idx, col.x, col.y, col.z, 1.0f);
+  if (COUNT) {
+    F.sdf_counts[idx] = c.march + c.reflect + c.shadow + 4u * c.normals;
+    flush_counts(F, c);
+  }
+}
+
+// main glsl:291-344 with 4x supersampling: one lane per (pixel, sample), the 4
+// samples of a pixel in adjacent lanes, summed in the reference's order
+// ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
+template <bool COUNT>
+__global__ __launch_bounds__(64) void k_table_sample(Frame F) {
+  extern __shared__ float lds[];
+  const Table S = stage(F, lds);
+  const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
+  const int by = tile_row(blockIdx.y, gridDim.y);
+  const int bx = tile_col(blockIdx.x, gridDim.x, 8);
+  const int px = bx * 4 + (q & 3);
+  const int lrow = by * 4 + (q >> 2);
+  if (px >= F.width || lrow >= F.rows) return;  // the 4 lanes of a pixel leave together
+  const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
+  const int py = global_row(F, lrow);
+  TCnt c = {0, 0, 0, 0, 0, 0};
+  f3 col = mk(0.0f, 0.0f, 0.0f);
+  if (py >= 0) {
+    f3 ro, rd;
+    cast_ray(F, F.uvx[px * 5 + 1 + s], F.uvy[py * 5 + 1 + s], ro, rd);
+    if (COUNT) c.rays++;
+    col = trender<COUNT>(F, S, ro, rd, c);
+  }
+  const float r1 = __shfl(col.x, lane + 1), g1 = __shfl(col.y, lane + 1), b1 = __shfl(col.z, lane + 1);
+  const float r2 = __shfl(col.x, lane + 2), g2 = __shfl(col.y, lane + 2), b2 = __shfl(col.z, lane + 2);
+  const float r3 = __shfl(col.x, lane + 3), g3 = __shfl(col.y, lane + 3), b3 = __shfl(col.z, lane + 3);
+  uint32_t cnt = 0;
+  if (COUNT) {
+    const uint32_t mine = c.march + c.reflect + c.shadow + 4u * c.normals;
+    cnt = mine + __shfl(mine, lane + 1) + __shfl(mine, lane + 2) + __shfl(mine, lane + 3);
+    flush_counts(F, c);
+  }
+  if (s != 0) return;
+  if (py >= 0) {
+    const float o0 = ((col.x + r1) + r2) + r3, o1 = ((col.y + g1) + g2) + g3,
+                o2 = ((col.z + b1) + b2) + b3;
+    store_pixel(F, idx, o0 / 4.0f, o1 / 4.0f, o2 / 4.0f, 1.0f);
+  } else {
+    store_pixel(F, idx, 0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  if (COUNT) F.sdf_counts[idx] = cnt;
+}
+
+}  // namespace rmd
+
+namespace rm {
+
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s) {
+  const size_t lds = RM_TABLE_LDS ? (size_t)F.nprims * TABLE_WORDS * sizeof(float) : 0;
+  if (F.aa) {
+    const dim3 g((F.width + 3) / 4, (F.rows + 3) / 4);
+    if (counters)
+      hipLaunchKernelGGL(rmd::k_table_sample<true>, g, dim3(64), lds, s, F);
+    else
+      hipLaunchKernelGGL(rmd::k_table_sample<false>, g, dim3(64), lds, s, F);
+  } else {
+    const dim3 g((F.width + 7) / 8, (F.rows + 7) / 8);
+    if (counters)
+      hipLaunchKernelGGL(rmd::k_table_pixel<true>, g, dim3(64), lds, s, F);
+    else
+      hipLaunchKernelGGL(rmd::k_table_pixel<false>, g, dim3(64), lds, s, F);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace rm

@@ -97,6 +97,39 @@ class rm_input_state(C.Structure):
                 ("mouseSensitivity", C.c_float), ("shouldClose", C.c_int32)]
 
 
+class rm_primitive(C.Structure):
+    _fields_ = [("type", C.c_int32), ("swizzle", C.c_int32), ("id", C.c_int32),
+                ("paint", C.c_int32), ("material", C.c_float), ("color", C.c_float * 3),
+                ("center", C.c_float * 3), ("param", C.c_float * 7)]
+
+
+# runtime scene table (include/rm_api.h)
+RM_MAX_PRIMITIVES = 32
+PRIM_SPHERE, PRIM_BOX, PRIM_BLEND, PRIM_TORUS, PRIM_CAPSULE, PRIM_PLANE = range(6)
+SWIZZLE_XYZ, SWIZZLE_XZY = 0, 1
+PAINT_SOLID, PAINT_CHECKERS = 0, 1
+REFLECTIVE, MATTE = 1.0, 0.0
+
+
+def primitive(type: int, center=(0.0, 0.0, 0.0), param=(), color=(1.0, 1.0, 1.0), id: int = 0,
+              material: float = REFLECTIVE, swizzle: int = SWIZZLE_XYZ,
+              paint: int = PAINT_SOLID) -> rm_primitive:
+    """One scene-table entry (a RayHit-producing primitive, glsl:83-121)."""
+    p = rm_primitive(type=type, swizzle=swizzle, id=id, paint=paint, material=material)
+    p.color[:] = list(color)
+    p.center[:] = list(center)
+    p.param[:] = list(param) + [0.0] * (7 - len(param))
+    return p
+
+
+def default_scene() -> list:
+    """The reference's scene (glsl:107-123) as table entries."""
+    n = C.c_int32(0)
+    out = (rm_primitive * RM_MAX_PRIMITIVES)()
+    _check(lib().rm_default_scene(out, RM_MAX_PRIMITIVES, C.byref(n)))
+    return [out[i] for i in range(n.value)]
+
+
 # GLFW key / action codes (glfw3.h) and held-key bits, as in include/rm_api.h
 KEY_A, KEY_D, KEY_L, KEY_S, KEY_W = 65, 68, 76, 83, 87
 KEY_ESCAPE, KEY_DOWN, KEY_UP, KEY_F1 = 256, 264, 265, 290
@@ -158,6 +191,9 @@ _SIGS = {
     "rm_input_euler_angles": (C.c_int, [C.POINTER(rm_input_state), C.POINTER(C.c_float)]),
     "rm_input_to_uniforms": (C.c_int, [C.POINTER(rm_input_state), C.POINTER(rm_camera_state),
                                        C.POINTER(rm_uniforms)]),
+    "rm_default_scene": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
+    "rm_set_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32]),
+    "rm_get_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(rm_uniforms)]),
 }
@@ -392,6 +428,20 @@ class Renderer:
         if y is None:
             x, y, z, w = x
         return _check(lib().rm_set_vec4(self._h, name.encode(), x, y, z, w), self._h)
+
+    def set_scene(self, prims: Optional[Sequence[rm_primitive]]) -> None:
+        """Render a runtime scene table from the next dispatch on (None: built-in scene)."""
+        if prims is None:
+            _check(lib().rm_set_scene(self.handle, None, 0), self.handle)
+            return
+        tbl = (rm_primitive * len(prims))(*prims)
+        _check(lib().rm_set_scene(self.handle, tbl, len(prims)), self.handle)
+
+    def get_scene(self) -> list:
+        n = C.c_int32(0)
+        out = (rm_primitive * RM_MAX_PRIMITIVES)()
+        _check(lib().rm_get_scene(self.handle, out, RM_MAX_PRIMITIVES, C.byref(n)), self.handle)
+        return [out[i] for i in range(n.value)]
 
     def set_uniforms(self, u: rm_uniforms) -> None:
         _check(lib().rm_set_uniforms(self._h, C.byref(u)), self._h)

@@ -19,7 +19,7 @@ _ROOT = os.path.dirname(_HERE)
 ORACLE_SO = os.path.join(_HERE, "_build", "librm_oracle.so")
 
 sys.path.insert(0, os.path.join(_ROOT, "opengl-raymarching-in-compute-shader_amd"))
-from rmarch import rm_counters, rm_uniforms  # noqa: E402  (shared POD structs)
+from rmarch import rm_counters, rm_primitive, rm_uniforms  # noqa: E402  (shared POD structs)
 
 
 class rmo_hit(C.Structure):
@@ -48,6 +48,11 @@ def lib() -> C.CDLL:
         L.rmo_render.argtypes = [_PU, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.POINTER(rm_counters),
                                  C.POINTER(rm_counters), C.c_int32]
+        L.rmo_render_scene.restype = C.c_int
+        L.rmo_render_scene.argtypes = [_PU, C.POINTER(rm_primitive), C.c_int32, C.c_int32,
+                                       C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.POINTER(rm_counters),
+                                       C.POINTER(rm_counters), C.c_int32]
         L.rmo_sdf.argtypes = [_PU, _F3, C.POINTER(rmo_hit)]
         L.rmo_raymarch.argtypes = [_PU, _F3, _F3, C.c_int32, C.POINTER(rmo_hit),
                                    C.POINTER(C.c_uint32)]
@@ -67,19 +72,26 @@ def lib() -> C.CDLL:
 
 
 def render(u: rm_uniforms, W: int, H: int, rows: Optional[Sequence[int]] = None,
-           nthreads: int = 0, want_f32: bool = True, want_counts: bool = True) -> dict:
-    """Render rows (default: all) with the oracle.  Row 0 = bottom (py = 0)."""
+           nthreads: int = 0, want_f32: bool = True, want_counts: bool = True,
+           scene: Optional[Sequence[rm_primitive]] = None) -> dict:
+    """Render rows (default: all) with the oracle.  Row 0 = bottom (py = 0).
+
+    ``scene``: a runtime scene table (rm_primitive entries) in place of the GLSL's
+    own sdf() (rmo_render_scene)."""
     n = H if rows is None else len(rows)
     rows_arr = None if rows is None else np.ascontiguousarray(rows, np.int32)
     rgba8 = np.zeros((n, W, 4), np.uint8)
     f32 = np.zeros((n, W, 4), np.float32) if want_f32 else None
     counts = np.zeros((n, W), np.uint32) if want_counts else None
     cnt, full = rm_counters(), rm_counters()
-    rc = lib().rmo_render(C.byref(u), W, H,
-                          None if rows_arr is None else rows_arr.ctypes.data, n,
-                          None if f32 is None else f32.ctypes.data, rgba8.ctypes.data,
-                          None if counts is None else counts.ctypes.data, C.byref(cnt),
-                          C.byref(full), nthreads)
+    tail = (W, H, None if rows_arr is None else rows_arr.ctypes.data, n,
+            None if f32 is None else f32.ctypes.data, rgba8.ctypes.data,
+            None if counts is None else counts.ctypes.data, C.byref(cnt), C.byref(full), nthreads)
+    if scene is None:
+        rc = lib().rmo_render(C.byref(u), *tail)
+    else:
+        tbl = (rm_primitive * len(scene))(*scene)
+        rc = lib().rmo_render_scene(C.byref(u), tbl, len(scene), *tail)
     if rc != 0:
         raise ValueError("rmo_render: bad arguments")
     return {"rgba8": rgba8, "rgba32f": f32, "sdf_counts": counts, "counters": cnt.as_dict(),

@@ -88,10 +88,14 @@ typedef struct rctx {
   const rm_uniforms *u;
   float blend;
   float k;
+  const rm_primitive *prims; /* runtime scene table (NULL: the GLSL's own scene) */
+  int nprims;
 } rctx;
 
 static void rctx_init(rctx *r, const rm_uniforms *u) {
   r->u = u;
+  r->prims = NULL;
+  r->nprims = 0;
   r->blend = sinf(u->iTime) / 2.0f + 0.5f;
   /* 2.0 at glsl:185,236; the hard-shadow extension is k = +inf. */
   r->k = u->shadow_mode == RM_SHADOW_HARD ? INFINITY : 2.0f;
@@ -138,8 +142,41 @@ static inline float sdCapsule(v3 p, v3 a, v3 b, float r) {
 /* glsl:105  (d1 < d2) ? d1 : d2  — ties keep d2 */
 static inline hit opU(hit d1, hit d2) { return (d1.hitpoint < d2.hitpoint) ? d1 : d2; }
 
+/* One runtime-table entry as a RayHit: the GLSL primitive
+ * of its type at q = (pos - center) (.xzy when swizzled, as glsl:119 does for
+ * the torus), the entry's colour or checkers(pos), id and material. */
+static hit table_entry(const rctx *R, const rm_primitive *P, v3 pos) {
+  v3 q = sub(pos, L3(P->center));
+  if (P->swizzle == RM_SWIZZLE_XZY) q = V(q.x, q.z, q.y);
+  const float *a = P->param;
+  float d;
+  switch (P->type) {
+    case RM_PRIM_SPHERE: d = sdSphere(q, a[0]); break;
+    case RM_PRIM_BOX: d = sdBox(q, V(a[0], a[1], a[2])); break;
+    case RM_PRIM_BLEND: { /* glsl:115-117: mix(Box, Sphere, sin(iTime)/2 + 0.5) */
+      float bx = sdBox(q, V(a[0], a[1], a[2]));
+      float sp = sdSphere(q, a[3]);
+      d = bx * (1.0f - R->blend) + sp * R->blend;
+      break;
+    }
+    case RM_PRIM_TORUS: d = sdTorus(q, a[0], a[1]); break;
+    case RM_PRIM_CAPSULE: d = sdCapsule(q, V(a[0], a[1], a[2]), V(a[3], a[4], a[5]), a[6]); break;
+    default: d = sdPlane(q, a[0], a[1], a[2], a[3]); break;
+  }
+  v3 col = P->paint == RM_PAINT_CHECKERS ? checkers(pos) : L3(P->color);
+  return H(d, col, P->id, P->material);
+}
+
+/* sdf() over a runtime table: the opU chain of glsl:110-122 in table order. */
+static hit sdf_table(const rctx *R, v3 pos) {
+  hit t = table_entry(R, &R->prims[0], pos);
+  for (int k = 1; k < R->nprims; k++) t = opU(t, table_entry(R, &R->prims[k], pos));
+  return t;
+}
+
 /* glsl:107-123 */
 static hit sdf(const rctx *R, v3 pos) {
+  if (R->nprims) return sdf_table(R, pos);
   hit t;
   t = H(sdSphere(sub(pos, V(15.0f, 0.0f, -10.0f)), 3.0f), V(0.1804f, 0.6f, 0.2157f), 0,
         REFLECTIVE);
@@ -375,15 +412,39 @@ static void tally_out(const tally *t, rm_counters *o) {
   o->sdf_evals = t->march + t->reflect + t->shadow + 4 * t->normals;
 }
 
+static int render_rows(const rctx *R, int32_t W, int32_t Hh, const int32_t *rows, int32_t nrows,
+                       float *rgba32f, uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
+                       rm_counters *full_counters, int32_t nthreads);
+
 int rmo_render(const rm_uniforms *u, int32_t W, int32_t Hh, const int32_t *rows, int32_t nrows,
                float *rgba32f, uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
                rm_counters *full_counters, int32_t nthreads) {
-  if (!u || W <= 0 || Hh <= 0) return -1;
-  int32_t n = rows ? nrows : Hh;
-  if (n < 0) return -1;
+  if (!u) return -1;
   rctx Rc;
   rctx_init(&Rc, u);
-  const rctx *R = &Rc;
+  return render_rows(&Rc, W, Hh, rows, nrows, rgba32f, rgba8, sdf_counts, counters, full_counters,
+                     nthreads);
+}
+
+int rmo_render_scene(const rm_uniforms *u, const rm_primitive *prims, int32_t nprims, int32_t W,
+                     int32_t Hh, const int32_t *rows, int32_t nrows, float *rgba32f,
+                     uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
+                     rm_counters *full_counters, int32_t nthreads) {
+  if (!u || !prims || nprims < 1 || nprims > RM_MAX_PRIMITIVES) return -1;
+  rctx Rc;
+  rctx_init(&Rc, u);
+  Rc.prims = prims;
+  Rc.nprims = nprims;
+  return render_rows(&Rc, W, Hh, rows, nrows, rgba32f, rgba8, sdf_counts, counters, full_counters,
+                     nthreads);
+}
+
+static int render_rows(const rctx *R, int32_t W, int32_t Hh, const int32_t *rows, int32_t nrows,
+                       float *rgba32f, uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
+                       rm_counters *full_counters, int32_t nthreads) {
+  if (W <= 0 || Hh <= 0) return -1;
+  int32_t n = rows ? nrows : Hh;
+  if (n < 0) return -1;
   tally live = {0, 0, 0, 0, 0, 0}, all = {0, 0, 0, 0, 0, 0};
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();

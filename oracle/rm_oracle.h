@@ -45,6 +45,14 @@ int rmo_render(const rm_uniforms *u, int32_t W, int32_t H, const int32_t *rows, 
                float *rgba32f, uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
                rm_counters *full_counters, int32_t nthreads);
 
+/* rmo_render with the runtime scene table prims[0..nprims) in place of the
+ * GLSL's own sdf(): the same primitives and opU rule,
+ * in table order.  Returns -1 on bad arguments. */
+int rmo_render_scene(const rm_uniforms *u, const rm_primitive *prims, int32_t nprims, int32_t W,
+                     int32_t H, const int32_t *rows, int32_t nrows, float *rgba32f,
+                     uint8_t *rgba8, uint32_t *sdf_counts, rm_counters *counters,
+                     rm_counters *full_counters, int32_t nthreads);
+
 /* Single-function entry points for known-answer tests (all follow the GLSL
  * line-for-line; see rm_oracle.c for the per-function citations). */
 typedef struct rmo_hit {

@@ -1,0 +1,80 @@
+"""Runtime scene table, host side: the reference scene as a
+table (rm_default_scene, computeShader.glsl:107-123) and the oracle's table mode.
+
+The oracle's table mode evaluates the same GLSL primitives (glsl:83-103) in table
+order with opU (glsl:105).  Fed the default table it must reproduce the oracle's
+literal transcription of sdf() bit for bit — colours, NaN masks and work counters —
+which pins the table semantics (entry order, swizzle, blend, checkers paint, ids,
+materials) to the reference scene.  No GPU calls."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+
+def test_default_scene_is_the_reference_scene(rm):
+    sc = rm.default_scene()
+    assert [p.type for p in sc] == [rm.PRIM_SPHERE, rm.PRIM_SPHERE, rm.PRIM_BLEND, rm.PRIM_TORUS,
+                                    rm.PRIM_CAPSULE, rm.PRIM_PLANE]
+    assert [p.id for p in sc] == [0, 1, 4, 5, 6, 7]                       # glsl:111-121
+    assert [p.material for p in sc] == [1.0] * 5 + [0.0]                  # REFLECTIVE.., MATTE
+    assert sc[3].swizzle == rm.SWIZZLE_XZY                                # (pos - c).xzy, :119
+    assert sc[5].paint == rm.PAINT_CHECKERS                               # checkers(pos), :121
+    assert list(sc[0].center) == [15.0, 0.0, -10.0] and sc[0].param[0] == 3.0
+    assert list(sc[2].param)[:4] == [3.0, 2.5, 2.5, 3.0]                  # box (3,2.5,2.5), r 3
+    f = lambda x: float(np.float32(x))
+    assert list(sc[4].param) == [f(-0.1), f(0.1), f(-0.1), 2.0, 4.0, 2.0, 1.0]
+    assert list(sc[5].param)[:4] == [0.0, 1.0, 0.0, 5.5]
+    assert [round(c, 4) for c in sc[1].color] == [0.0, 0.851, 1.0]
+
+
+def test_default_scene_capacity(rm):
+    n = C.c_int32(0)
+    assert rm.lib().rm_default_scene(None, 0, C.byref(n)) == 0 and n.value == 6
+    small = (rm.rm_primitive * 5)()
+    assert rm.lib().rm_default_scene(small, 5, C.byref(n)) == rm.RM_ERR_INVALID
+    assert C.sizeof(rm.rm_primitive) == 72
+
+
+@pytest.mark.parametrize("frame,bounces,aa,shadow", [
+    (0, 3, True, 0), (40, 5, False, 0), (119, 1, True, 1), (-1, 2, True, 0), (77, 0, False, 0)])
+def test_oracle_table_mode_equals_the_glsl_scene(rm, oracle, frame, bounces, aa, shadow):
+    u = rm.sweep_uniforms(frame, 120, bounces, aa, shadow)
+    a = oracle.render(u, 64, 40)
+    b = oracle.render(u, 64, 40, scene=rm.default_scene())
+    np.testing.assert_array_equal(a["rgba32f"], b["rgba32f"])  # NaN == NaN here
+    assert a["counters"] == b["counters"] and a["full_counters"] == b["full_counters"]
+    np.testing.assert_array_equal(a["sdf_counts"], b["sdf_counts"])
+
+
+def test_far_entries_change_nothing(rm, oracle):
+    # an entry that is never the minimum leaves every sdf() value and id unchanged
+    far = rm.primitive(rm.PRIM_SPHERE, (0.0, 5000.0, 0.0), (1.0,), (1, 0, 0), id=9)
+    sc = rm.default_scene()
+    u = rm.sweep_uniforms(30, 120, 2, False, 0)
+    a = oracle.render(u, 48, 32, scene=sc)
+    b = oracle.render(u, 48, 32, scene=sc + [far])
+    c = oracle.render(u, 48, 32, scene=[far] + sc)
+    np.testing.assert_array_equal(a["rgba32f"], b["rgba32f"])
+    np.testing.assert_array_equal(a["rgba32f"], c["rgba32f"])
+
+
+def test_scene_changes_the_image(rm, oracle):
+    u = rm.sweep_uniforms(30, 120, 1, False, 0)
+    sc = rm.default_scene()
+    moved = rm.default_scene()
+    moved[0].center[1] = 2.0                    # lift the green sphere
+    a = oracle.render(u, 48, 32, scene=sc)["rgba8"]
+    b = oracle.render(u, 48, 32, scene=moved)["rgba8"]
+    assert (a != b).any()
+
+
+def test_oracle_rejects_bad_tables(rm, oracle):
+    u = rm.sweep_uniforms(0)
+    out = np.zeros((4, 4, 4), np.uint8)
+    L = oracle.lib()
+    assert L.rmo_render_scene(C.byref(u), None, 0, 4, 4, None, 4, None, out.ctypes.data, None,
+                              None, None, 1) == -1
+    tbl = (rm.rm_primitive * 33)()
+    assert L.rmo_render_scene(C.byref(u), tbl, 33, 4, 4, None, 4, None, out.ctypes.data, None,
+                              None, None, 1) == -1
