@@ -39,7 +39,17 @@ struct TCnt {
 
 using rm::TABLE_WORDS;
 
-__device__ __forceinline__ float isqrt_ieee(float x) { return __builtin_sqrtf(x); }
+#ifndef RM_TABLE_FAST_SQRT
+#define RM_TABLE_FAST_SQRT 0
+#endif
+// Correctly rounded sqrt of a sum of squares (x >= 0, +inf or NaN).  The fast
+// form is sqrt_cr_nonneg (exact on [0, FLT_MAX], rm_fastmath.hpp) with +inf
+// passed through, so it equals the IEEE sqrt on the whole domain.
+__device__ __forceinline__ float isqrt_ieee(float x) {
+  if (!RM_TABLE_FAST_SQRT) return __builtin_sqrtf(x);
+  const float s = sqrt_cr_nonneg(x);
+  return x == __builtin_inff() ? x : s;
+}
 __device__ __forceinline__ float tlen(f3 a) { return isqrt_ieee(dot(a, a)); }
 // GLSL normalize over the full float range (v * (1 / sqrt(dot)))
 __device__ __forceinline__ f3 tnormalize(f3 a) { return muls(a, 1.0f / isqrt_ieee(dot(a, a))); }
