@@ -185,7 +185,22 @@ int check_uniforms(rm_ctx* c, const rm_uniforms& u) {
 
 }  // namespace
 
+#ifdef RM_STATS
+namespace rm {
+hipError_t debug_stats(unsigned long long* out, bool clear);
+}
+#endif
+
 extern "C" {
+
+#ifdef RM_STATS
+/* Diagnostic builds only (-DRM_STATS, tools/build_variant.sh): the 64 wave /
+ * lane counters of rm_scene.hpp's RM_STAT points, then cleared. */
+int rm_debug_stats(unsigned long long *out64) {
+  return rm::debug_stats(out64, true) == hipSuccess ? 0 : -1;
+}
+#endif
+
 
 const char* rm_last_error(const rm_ctx* ctx) {
   return ctx ? ctx->err.c_str() : g_create_error.c_str();

@@ -23,6 +23,9 @@
 #ifndef RM_PRIMARY_PREP
 #define RM_PRIMARY_PREP 1
 #endif
+#ifndef RM_MARCH_V2
+#define RM_MARCH_V2 1
+#endif
 
 namespace rmd {
 
@@ -119,6 +122,42 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     i0 = 2;
   }
 #endif
+#if RM_MARCH_V2 && RM_LAZY_CULL && RM_MISS_EXIT && !defined(RM_STATS)
+  if (!COUNT) {
+    // Production loop.  A lane leaves on hit | escape | proven miss, folded by
+    // VALU selects into one compare (a NaN probe fails `<=`, so does a finite
+    // t + d past the exit threshold; mx may be +inf); the 512 / 256 step cap is
+    // the same step for every lane of the wave (all start at i0), so it is a
+    // scalar loop bound.  The result is carried as a VGPR (t on a hit, else -1)
+    // instead of a lane mask.  A NaN distance (degenerate scenes) leaves at
+    // once: the reference marches on with t = NaN to the cap, also a miss.
+    float tres = -1.0f;
+    const float QNAN = __builtin_nanf("");
+    for (int i = i0;; ++i) {
+      const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+      const bool h = d < 0.000001f * t;
+      tres = h ? t : -1.0f;
+      asm volatile("" : "+v"(tres));  // a VGPR live-out, not a lane mask
+      dl = d;
+      const float tn = t + d;
+      float probe = h ? QNAN : tn;
+      probe = (d > tmax) ? QNAN : probe;
+      if (!(probe <= mx)) break;
+      t = tn;
+      if (i >= nmax) break;
+    }
+    if (tres >= 0.0f) {
+      const f3 q = add(ro, muls(rd, tres));
+      id = lazy_id(lc, tres);
+      col = hit_color(id, q);
+      dlast = dl;
+      return tres;
+    }
+    id = -1;
+    col = mk(0.0f, 0.0f, 0.0f);
+    return -1.0f;
+  }
+#endif
   // One exit per step (hit | escape | step cap | proven miss), tested with
   // VALU: a single exec-mask update per iteration.
 #ifdef RM_STATS
@@ -132,7 +171,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       if (__lane_id() == __builtin_ffsll(m) - 1) {
         atomicAdd(&g_stats[reflected ? 6 : 15], 1ull);
         atomicAdd(&g_stats[7], (unsigned long long)__popcll(m));
-        atomicAdd(&g_stats[16 + (reflected ? 6 : 15)], (unsigned long long)__popcll(m));
+        atomicAdd(&g_stats[32 + (reflected ? 6 : 15)], (unsigned long long)__popcll(m));
       }
     }
 #endif
@@ -157,10 +196,10 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     if (stop) break;
   }
 #ifdef RM_STATS
-  // lane sums of steps: [4] primary miss, [5] primary hit, [20] reflected miss,
-  // [21] reflected hit; [12] / [13] count the primary miss / hit lanes
-  atomicAdd(&g_stats[(reflected ? 20 : 4) + (hit ? 1 : 0)], (unsigned long long)nst);
-  if (!reflected) atomicAdd(&g_stats[hit ? 13 : 12], 1ull);
+  // lane sums of steps: [4] primary miss, [5] primary hit, [24] reflected miss,
+  // [25] reflected hit; [3] / [23] count the primary miss / hit lanes
+  atomicAdd(&g_stats[(reflected ? 24 : 4) + (hit ? 1 : 0)], (unsigned long long)nst);
+  if (!reflected) atomicAdd(&g_stats[hit ? 23 : 3], 1ull);
 #endif
   if (hit) {
     // the opU id (and colour) of the hit: from the last step's sdf (same point)
@@ -566,6 +605,18 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
     hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
   return hipGetLastError();
 }
+
+#ifdef RM_STATS
+// Diagnostic builds: rm_debug_stats() (rm_api.hip) reads and clears g_stats.
+hipError_t debug_stats(unsigned long long* out, bool clear) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rmd::g_stats), 64 * sizeof(unsigned long long));
+  if (e == hipSuccess && clear) {
+    static const unsigned long long z[64] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_stats), z, sizeof z);
+  }
+  return e;
+}
+#endif
 
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s) {

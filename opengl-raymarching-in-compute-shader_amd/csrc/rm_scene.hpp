@@ -51,6 +51,18 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) {
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// max of two lazy-culling expiries (LazyCull::te): each is -inf or >= +0 (never
+// NaN: t >= 0 and the budgets are max'ed with t), a set on which the signed
+// integer order of the bit patterns is the float order -- one v_max_i32,
+// without the NaN-quieting canonicalisation LLVM puts around fmaxf of a phi.
+__device__ __forceinline__ float te_max(float a, float b) {
+  return __int_as_float(max(__float_as_int(a), __float_as_int(b)));
+}
 // GLSL min/max (y < x ? y : x) — used where a signed zero or NaN could differ.
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
@@ -117,15 +129,15 @@ constexpr float R_CAPSULE = 3.45115f;    // >= |b-a|/2 + 1 = sqrt(24.03)/2 + 1 =
 constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;  // segment midpoint
 
 #ifdef RM_STATS
-// Diagnostic build only: g_stats[k] counts waves reaching point k, g_stats[16+k]
-// the active lanes there.
-__device__ unsigned long long g_stats[32];
+// Diagnostic build only: g_stats[k] counts waves reaching point k, g_stats[32+k]
+// the active lanes there (k < 32).
+__device__ unsigned long long g_stats[64];
 #define RM_STAT(k)                                                   \
   do {                                                               \
     const unsigned long long m_ = __ballot(1);                       \
     if (__lane_id() == __builtin_ffsll(m_) - 1) {                    \
       atomicAdd(&g_stats[k], 1ull);                                  \
-      atomicAdd(&g_stats[16 + (k)], (unsigned long long)__popcll(m_)); \
+      atomicAdd(&g_stats[32 + (k)], (unsigned long long)__popcll(m_)); \
     }                                                                \
   } while (0)
 #else
@@ -433,6 +445,9 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
 #ifndef RM_LAZY_ALL
 #define RM_LAZY_ALL 0
 #endif
+#ifndef RM_TE_FMA
+#define RM_TE_FMA 1
+#endif
 #ifndef RM_LAZY_EXACT_TE
 #define RM_LAZY_EXACT_TE 0
 #endif
@@ -481,51 +496,60 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       m = vmin(m, v);
     };
     // re-test k; returns true when k must be evaluated exactly at this step
-    auto retest = [&](float x, float R, float& te) -> bool {
+    auto retest = [&](float x, float R, float& te, int k) -> bool {
       RM_STAT(1);
+      RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       const float g = lb - m - slack;
-      // g <= 0 makes both budgets <= 0 (plane >= m), so max(.., 0) is the
-      // "no budget" case; an expired te is <= t <= t + bud, so max(te, .)
-      // serves both the expired lane and the idle one
+      // g <= 0 makes both budgets <= 0 (plane >= m), so max(.., t) is the
+      // "no budget" case; an expired te is <= t, so max(te, .) serves both the
+      // expired lane and the idle one.  t + max(b1, b2, 0) == max(t + b1, t + b2, t)
+      // (rounding is monotone); the fmas round once instead of twice, inside the
+      // budgets' 2^-10 margin.
+#if RM_TE_FMA
+      const float tn = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), t);
+      const bool expired = t >= te;
+      te = te_max(te, tn);
+#else
       const float bud = __builtin_fmaxf(__builtin_fmaxf(g * inv2v, (lb - pl) * invp), 0.0f);
       const bool expired = t >= te;
       te = __builtin_fmaxf(te, t + bud);
+#endif
       return expired & !(g > 0.0f);
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
     if (RM_LZ_ANY(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
-      if (retest(x0, 3.0f, lc.te[0])) {
+      if (retest(x0, 3.0f, lc.te[0], 0)) {
         RM_STAT(10);
         take(sqrt_core(x0) - 3.0f, 0, lc.te[0]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
-      if (retest(x1, 3.0f, lc.te[1])) {
+      if (retest(x1, 3.0f, lc.te[1], 1)) {
         RM_STAT(11);
         take(sqrt_core(x1) - 3.0f, 1, lc.te[1]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
-      if (retest(xs, R_BLEND_LO, lc.te[2])) {
+      if (retest(xs, R_BLEND_LO, lc.te[2], 2)) {
         RM_STAT(12);
         take(sd_blend(o, xs, blend, omblend), 4, lc.te[2]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3])) {
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
         RM_STAT(13);
         take(sd_torus(o, tz), 5, lc.te[3]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4])) {
+      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4)) {
         RM_STAT(14);
         take(sd_capsule(o, p), 6, lc.te[4]);
       }
