@@ -20,6 +20,7 @@
 namespace rm {
 extern int g_wq_batch;
 extern int g_wq_blocks_per_cu;
+void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
@@ -135,6 +136,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.prep = c->d_prep;
   F.scene = c->nprims ? reinterpret_cast<const float*>(c->d_scene) : nullptr;
   F.nprims = c->nprims;
+  rm::pixel_grid(F.width, F.rows, F.aa != 0, &F.grid_x, &F.grid_y);
   return F;
 }
 

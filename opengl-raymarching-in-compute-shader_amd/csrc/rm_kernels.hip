@@ -9,6 +9,8 @@
 // See DESIGN.md §4 for the kernel designs and their rooflines.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rm_scene.hpp"
 
 #ifndef RM_LAZY_CULL
@@ -25,6 +27,9 @@
 #endif
 #ifndef RM_MARCH_V2
 #define RM_MARCH_V2 1
+#endif
+#ifndef RM_ESC_SPLIT
+#define RM_ESC_SPLIT 1
 #endif
 
 namespace rmd {
@@ -128,30 +133,41 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     // VALU selects into one compare (a NaN probe fails `<=`, so does a finite
     // t + d past the exit threshold; mx may be +inf); the 512 / 256 step cap is
     // the same step for every lane of the wave (all start at i0), so it is a
-    // scalar loop bound.  The result is carried as a VGPR (t on a hit, else -1)
-    // instead of a lane mask.  A NaN distance (degenerate scenes) leaves at
-    // once: the reference marches on with t = NaN to the cap, also a miss.
-    float tres = -1.0f;
+    // scalar loop bound.  t advances only when the lane goes on, so at the exit
+    // (t, dl) is the last step's pair and `dl < 1e-6 t` re-forms its hit test
+    // exactly.  A NaN distance (degenerate scenes) leaves at once: the
+    // reference marches on with t = NaN to the cap, also a miss.
+    //
+    // The escape test d > tmax is implied, for a lane, by either of
+    //   mx <= tmax:  d > tmax  =>  t + d >= d > tmax >= mx (t >= 0, rounding is
+    //                monotone): the proven-miss compare already fires, also a miss;
+    //   rd.y <= 0 and ro.y + 5.5 <= tmax:  d <= plane(t) = (ro.y + rd.y t) + 5.5
+    //                <= ro.y + 5.5 <= tmax: no step ever escapes.
+    // Only waves with a lane outside both cases run the loop with the test.
     const float QNAN = __builtin_nanf("");
-    for (int i = i0;; ++i) {
-      const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-      const bool h = d < 0.000001f * t;
-      tres = h ? t : -1.0f;
-      asm volatile("" : "+v"(tres));  // a VGPR live-out, not a lane mask
-      dl = d;
-      const float tn = t + d;
-      float probe = h ? QNAN : tn;
-      probe = (d > tmax) ? QNAN : probe;
-      if (!(probe <= mx)) break;
-      t = tn;
-      if (i >= nmax) break;
-    }
-    if (tres >= 0.0f) {
-      const f3 q = add(ro, muls(rd, tres));
-      id = lazy_id(lc, tres);
+    auto run = [&](auto esc) {
+      for (int i = i0;; ++i) {
+        const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+        const bool h = d < 0.000001f * t;
+        dl = d;
+        const float tn = t + d;
+        float probe = h ? QNAN : tn;
+        if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
+        if (!(probe <= mx)) break;
+        if (i >= nmax) break;
+        t = tn;
+      }
+    };
+    const bool need_esc = (mx > tmax) && !(rd.y <= 0.0f && ro.y + 5.5f <= tmax);
+    if (!RM_ESC_SPLIT || __any(need_esc)) run(std::true_type());
+    else run(std::false_type());
+    asm volatile("" : "+v"(t), "+v"(dl));  // re-form the test, not a lane mask kept per step
+    if (dl < 0.000001f * t) {
+      const f3 q = add(ro, muls(rd, t));
+      id = lazy_id(lc, t);
       col = hit_color(id, q);
       dlast = dl;
-      return tres;
+      return t;
     }
     id = -1;
     col = mk(0.0f, 0.0f, 0.0f);
@@ -401,8 +417,8 @@ constexpr int kTileH = kPixelWaves == 4 ? 16 : 8;
 template <bool COUNT>
 __device__ __forceinline__ void pixel_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int by = tile_row(blockIdx.y, gridDim.y);
-  const int bx = tile_col(blockIdx.x, gridDim.x, 128 / (kTileW * 4));
+  const int by = tile_row(blockIdx.y, F.grid_y);
+  const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kTileW * 4));
   const int px = bx * kTileW + (wave & 1) * 8 + (lane & 7);
   const int lrow = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
   if (px >= F.width || lrow >= F.rows) return;
@@ -468,8 +484,8 @@ template <bool COUNT>
 __device__ __forceinline__ void sample_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
-  const int by = tile_row(blockIdx.y, gridDim.y);
-  const int bx = tile_col(blockIdx.x, gridDim.x, 128 / (kSampleTileW * 4));
+  const int by = tile_row(blockIdx.y, F.grid_y);
+  const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kSampleTileW * 4));
   const int px = bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
   const int lrow = by * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
   if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
@@ -507,7 +523,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
   if (lane == 0) {
     unsigned hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    const size_t w = (size_t)by * gridDim.x + bx;
+    const size_t w = (size_t)by * F.grid_x + bx;
     g_wave_times[3 * w] = wt0;
     g_wave_times[3 * w + 1] = wall_clock64();
     g_wave_times[3 * w + 2] = hw;
@@ -587,18 +603,24 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
 // ---- launch wrappers used by rm_api.hip --------------------------------------
 namespace rm {
 
+void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy) {
+  *gx = aa ? (width + rmd::kSampleTileW - 1) / rmd::kSampleTileW : (width + rmd::kTileW - 1) / rmd::kTileW;
+  *gy = aa ? (rows + rmd::kSampleTileH - 1) / rmd::kSampleTileH : (rows + rmd::kTileH - 1) / rmd::kTileH;
+}
+
+// F.grid_x / grid_y must be pixel_grid(F.width, F.rows, F.aa) (make_frame): the
+// kernels read the grid from their arguments, not from the hidden dispatch
+// arguments, so the prologue's tile arithmetic waits for one round of loads.
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
   hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
+  const dim3 grid(F.grid_x, F.grid_y);
   if (F.aa) {
-    const dim3 g((F.width + rmd::kSampleTileW - 1) / rmd::kSampleTileW,
-                 (F.rows + rmd::kSampleTileH - 1) / rmd::kSampleTileH);
     if (counters)
-      hipLaunchKernelGGL(rmd::k_sample<true>, g, dim3(RM_SAMPLE_BLOCK), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<true>, grid, dim3(RM_SAMPLE_BLOCK), 0, s, F);
     else
-      hipLaunchKernelGGL(rmd::k_sample<false>, g, dim3(RM_SAMPLE_BLOCK), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<false>, grid, dim3(RM_SAMPLE_BLOCK), 0, s, F);
     return hipGetLastError();
   }
-  const dim3 grid((F.width + rmd::kTileW - 1) / rmd::kTileW, (F.rows + rmd::kTileH - 1) / rmd::kTileH);
   if (counters)
     hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
   else

@@ -95,6 +95,8 @@ struct Frame {
   const float* prep;     // step 0 of the primary rays (PrepSlot), written by k_prep
   const float* scene;    // runtime scene table (rm_set_scene), TABLE_WORDS per primitive, or null
   int32_t nprims;        // entries in `scene`
+  int32_t grid_x, grid_y;  // k_pixel / k_sample grid (rm::pixel_grid): ordinary kernel
+                           // arguments, loaded with the rest of the prologue's
 };
 
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
@@ -756,9 +758,8 @@ __device__ __forceinline__ int tile_row(int b, int n) {
 __device__ __forceinline__ int tile_col(int b, int gx, int G) {
   const int win = 8 * G;
   const int w0 = (b / win) * win;
-  if (w0 + win > gx) return b;  // ragged last window: natural order
   const int r = b - w0;
-  return w0 + (r & 7) * G + (r >> 3);
+  return (w0 + win > gx) ? b : w0 + (r & 7) * G + (r >> 3);  // ragged last window: natural order
 }
 
 // Global row of a launch-local row (row sharding).
