@@ -31,6 +31,15 @@
 #ifndef RM_ESC_SPLIT
 #define RM_ESC_SPLIT 1
 #endif
+#ifndef RM_CAP_EXIT
+#define RM_CAP_EXIT 1
+#endif
+#ifndef RM_CAP_I0
+#define RM_CAP_I0 16
+#endif
+#ifndef RM_CAP_I1
+#define RM_CAP_I1 64
+#endif
 
 namespace rmd {
 
@@ -99,6 +108,15 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #if RM_LAZY_CULL
   LazyCull lc;
   lazy_init(lc, rd, rdl, s0, s1);
+  // lin_exit's object bound T1 for the step-cap check, re-formed there from the
+  // ray (rare) rather than kept live through the loop
+  // (opaque: keeps the compiler from hoisting it, and its registers, out of the loop)
+  auto cap_T1 = [&](f3 o, f3 r) {
+    float b1c, b2c;
+    if (RM_PRIMARY_PREP && !reflected && F.prep[PREP_VALID] != 0.0f) b1c = F.prep[PREP_B1];
+    else lin_exit_b(o, lc.s0, 0.0f, b1c, b2c);
+    return lin_exit_T1(MISS_C, ray_rdl(r), lc.s1, b1c);
+  };
 #endif
   // provable miss (rm_scene.hpp "early exits"): production stops there; the
   // counting build runs on to the reference's step count and poisons the colour
@@ -146,16 +164,45 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     // Only waves with a lane outside both cases run the loop with the test.
     const float QNAN = __builtin_nanf("");
     auto run = [&](auto esc) {
-      for (int i = i0;; ++i) {
-        const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-        const bool h = d < 0.000001f * t;
-        dl = d;
-        const float tn = t + d;
-        float probe = h ? QNAN : tn;
-        if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
-        if (!(probe <= mx)) break;
-        if (i >= nmax) break;
-        t = tn;
+      // The march runs in segments ending at the scalar step indices of the
+      // step-cap check (RM_CAP_EXIT): the step loop itself is the plain one, with
+      // the segment end as its scalar bound.  Between segments a lane's exit test
+      // is re-formed from its last (t, dl) (same operations, same result), the
+      // lanes still marching take the check, and those that go on take the step.
+      int ib = i0, iend = RM_CAP_EXIT ? RM_CAP_I0 : nmax;
+      bool live = true;
+#pragma unroll 1
+      for (;;) {
+        if (live) {
+          for (int i = ib;; ++i) {
+            const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+            const bool h = d < 0.000001f * t;
+            dl = d;
+            const float tn = t + d;
+            float probe = h ? QNAN : tn;
+            if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
+            if (!(probe <= mx)) break;
+            if (i >= iend) break;
+            t = tn;
+          }
+        }
+        if (iend >= nmax) break;
+#if RM_CAP_EXIT
+        {
+          float probe = (dl < 0.000001f * t) ? QNAN : t + dl;
+          if (decltype(esc)::value) probe = (dl > tmax) ? QNAN : probe;
+          live = live && (probe <= mx);
+          // step-cap miss exit (rm_scene.hpp) for waves holding a grazing downward
+          // ray; K = nmax - iend evaluations would remain
+          if (__any(live && rd.y < 0.0f && rd.y > -0.05f)) {
+            const f3 o = opaque(ro), r = opaque(rd);
+            live = live && !cap_miss(t, dl, nmax - iend, o.y, r.y, cap_T1(o, r));
+          }
+          if (live) t = probe;
+        }
+#endif
+        ib = iend + 1;
+        iend = iend < RM_CAP_I1 ? RM_CAP_I1 : nmax;  // segments end at I0 < I1 < nmax
       }
     };
     const bool need_esc = (mx > tmax) && !(rd.y <= 0.0f && ro.y + 5.5f <= tmax);
@@ -203,6 +250,13 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     hit = d < 0.000001f * t;
     dl = d;
     bool stop = hit | (d > tmax) | (i >= nmax);
+#if RM_CAP_EXIT && RM_LAZY_CULL && RM_MISS_EXIT
+    if (i == RM_CAP_I0 || i == RM_CAP_I1) {  // same check as the production loop
+      const bool cm = !stop && cap_miss(t, d, nmax - i, ro.y, rd.y, cap_T1(ro, rd));
+      if (COUNT) proven_miss |= cm;
+      else stop |= cm;
+    }
+#endif
     t += stop ? 0.0f : d;  // t >= +0: t + 0 == t
     if (RM_MISS_EXIT) {
       const bool gone = !stop && lin_exit(mx, t);

@@ -635,6 +635,50 @@ __device__ __forceinline__ float shadow_exit_init(float k, f3 ro, f3 rd) {
 __device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd); }
 __device__ __forceinline__ bool lin_exit(float T, float t) { return t > T; }
 
+// ---- step-cap miss exit (RayMarch / reflectedRay, glsl:125-161) ---------------
+// A march that spends its nmax steps without a hit is a miss (glsl:141,160), as
+// is an escape; a miss discards t.  Downward rays grazing the floor toward the
+// horizon approach the plane geometrically and many reach the cap: with every
+// object provably above the hit threshold, the plane distance P(t) = ro.y + 5.5
+// + rd.y t (exact real; rd.y < 0, q = 1 + rd.y in (0.5, 1)) shrinks by at most
+// the factor q per step.  Let u = 2^-24 and, for a ray above the floor (P0 =
+// ro.y + 5.5 > 0), Tb >= P0 / |rd.y| + slack the largest t reached while P > 0.
+//   * the computed plane h = RN(RN(RN(rd.y t) + ro.y) + 5.5) is within
+//     E1 = 2^-21 (|ro.y| + 5.5) >= 5u (|ro.y| + 5.5)(1 + u) of P(t), t <= Tb;
+//   * a step moves t by  RN(t + d) - t <= d + u Tb <= h + u Tb  (d = min(h,
+//     objects) <= h), so  P' >= P - |rd.y| (P + E1 + u Tb) = q P - |rd.y| E2,
+//     E2 = E1 + 2u Tb, and over k steps (|rd.y| sum q^j <= 1)  P_k >= q^k P - E2;
+//   * a hit needs d < RN(1e-6 t) <= thr = 1e-6 Tb (1 + 2^-20); objects are above
+//     MISS_C t > thr once t > T1 (lin_exit_T1), so a hit needs h < thr, i.e.
+//     P < thr + E1;
+//   * P_n >= d_n - E1 at the current step (its hit test failed).
+// Hence, at step i with K = nmax - i evaluations left and t > T1, if
+//   (d - E1) q^K >= A = (thr + E1 + E2)(1 + 2^-10)
+// then P stays above thr + E1 > 0 (so t < Tb, closing the induction) on every
+// remaining step: no step hits and the march ends in a miss.  q^K is bounded
+// below with v_log / v_exp and relative (2^-12) plus absolute (2^-20 in the
+// exponent) margins far above their errors; NaNs fail the compare (no exit).
+// Only rays with -0.05 < rd.y < 0 can pass (q^K |rd.y| >= 1e-6 needs it for K
+// >= 240), so the check runs behind that wave-uniform test.
+__device__ __forceinline__ float lin_exit_T1(float c, float rdl, float s1, float b1) {
+  const float LO = 1.0f - 0x1p-12f;
+  const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
+  const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * (1.0f + 0x1p-20f);
+  return a1 > 0.0f ? T1 : __builtin_huge_valf();
+}
+__device__ __forceinline__ bool cap_miss(float t, float d, int K, float roy, float rdy, float T1) {
+  const float P0 = (roy + 5.5f) * (1.0f + 0x1p-22f);  // >= ro.y + 5.5 when that is > 0
+  const float nr = -rdy;
+  const float Tb = __builtin_fmaf(P0 * __builtin_amdgcn_rcpf(nr), 1.0f + 0x1p-20f, 0x1p-10f);
+  const float E1 = 0x1p-21f * (fabsf(roy) + 5.5f);
+  const float E2 = __builtin_fmaf(0x1p-23f, Tb, E1);
+  const float A = ((0.000001f * (1.0f + 0x1p-20f)) * Tb + E1 + E2) * (1.0f + 0x1p-10f);
+  const float q = (1.0f + rdy) - 0x1p-23f;  // < 1 + rd.y
+  const float L = __builtin_fmaf(__builtin_amdgcn_logf(q), 1.0f + 0x1p-12f, -0x1p-20f);  // < log2 q
+  const float qK = __builtin_amdgcn_exp2f((float)K * L) * (1.0f - 0x1p-12f);          // < q^K
+  return (rdy < 0.0f) & (rdy > -0.5f) & (P0 > 0.0f) & (t > T1) & ((d - E1) * qK >= A);
+}
+
 // softshadow's  res = min(res, k * h / t)  (glsl:211), exactly.  The quotient
 // only matters when it is below res, so it is first bounded with v_rcp_f32
 // (within 1 ulp): if (k*h)*rcp(t) exceeds res by a 2^-16 relative margin the

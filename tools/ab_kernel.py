@@ -1,0 +1,72 @@
+"""Interleaved A/B of kernel time per frame: librm.so and tools/variants/librm_*.so.
+
+  python tools/ab_kernel.py [--cfg 3] [--rounds 4] [--frames 30] [variant.so ...]
+
+Each (round, variant) runs in its own process (RM_LIBRM selects the library);
+the variants alternate within every round, so box drift hits them alike.  Each
+run renders `frames` sweep frames one at a time (HIP events on the context's
+stream) and reports the mean kernel ms per frame; the summary is the median
+over rounds.  Diagnostic tool, not part of the product.
+"""
+import argparse
+import glob
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFGS = {1: (512, 512, 0, False, 1), 2: (1920, 1080, 1, False, 0), 3: (3840, 2160, 3, True, 0),
+        4: (3840, 2160, 5, True, 0), 5: (7680, 4320, 3, True, 0)}
+
+
+def child(cfg, frames):
+    sys.path.insert(0, os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd"))
+    import rmarch as rm
+
+    W, H, b, aa, sm = CFGS[cfg]
+    with rm.Renderer(W, H) as r:
+        r.enable_timing(True)
+        for f in range(3):
+            r.dispatch(rm.sweep_uniforms(f, 120, b, aa, sm))
+        r.kernel_time_ms(reset=True)
+        for k in range(frames):
+            r.dispatch(rm.sweep_uniforms((k * 120) // frames, 120, b, aa, sm))
+        ms, n = r.kernel_time_ms(reset=True)
+    print(json.dumps({"ms": ms / n}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("libs", nargs="*")
+    a = ap.parse_args()
+    if a.child:
+        return child(a.cfg, a.frames)
+    libs = a.libs or ([os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd/librm.so")]
+                      + sorted(p for p in glob.glob(os.path.join(ROOT, "tools/variants/librm_*.so"))
+                               if "librm_stats" not in p))
+    res = {p: [] for p in libs}
+    for _ in range(a.rounds):
+        for p in libs:
+            env = dict(os.environ, RM_LIBRM=p)
+            out = subprocess.run([sys.executable, __file__, "--child", "--cfg", str(a.cfg), "--frames",
+                                  str(a.frames)], env=env, capture_output=True, text=True, timeout=120)
+            if out.returncode != 0:
+                sys.stderr.write(out.stderr)
+                sys.exit(out.returncode)
+            res[p].append(json.loads(out.stdout.strip().splitlines()[-1])["ms"])
+    base = statistics.median(res[libs[0]])
+    for p in libs:
+        m = statistics.median(res[p])
+        print("cfg%d %-28s median %.4f ms (%+.2f%%)  runs %s" % (
+            a.cfg, os.path.basename(p), m, 100.0 * (m / base - 1.0), " ".join("%.4f" % x for x in res[p])),
+            flush=True)
+
+
+if __name__ == "__main__":
+    main()
