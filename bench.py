@@ -122,7 +122,7 @@ def main() -> int:
                     help="N > 1: gather frame f on a second stream while frame f+1 renders "
                          "(double-buffered shard images); 0 = render, gather, assemble in turn")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-stride", type=int, default=4,
+    ap.add_argument("--cpu-row-stride", type=int, default=2,
                     help="cpu_baseline renders every k-th row of one frame")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     args = ap.parse_args()
@@ -314,7 +314,8 @@ def main() -> int:
         cpu = {"value": round(len(rows) * W / (c1 - c0) / 1e6, 4), "unit": "Mpixels/s",
                "cores": threads, "kind": "port",
                "sample": f"rows py%{args.cpu_row_stride}==0 of sweep frame {f} "
-                         f"({len(rows)}x{W} px, {cfg['desc']}), {c1 - c0:.2f}s wall"}
+                         f"({len(rows)}x{W} px, {cfg['desc']}), {c1 - c0:.2f}s wall, "
+                         f"{(c1 - c0) * threads:.0f} core-s"}
         # GPU frame of the same sweep frame: the last step rendered it into its context's buffer.
         torch.cuda.synchronize()
         g = outs[(args.warmup + args.steps - 1) % nfl].cpu().numpy()[rows]

@@ -37,6 +37,9 @@
 #ifndef RM_CAP_I0
 #define RM_CAP_I0 16
 #endif
+#ifndef RM_CAP_REFL
+#define RM_CAP_REFL 0  // 1: the check in reflected marches too (5 VGPR spills, +24 MB scratch writes)
+#endif
 #ifndef RM_CAP_I1
 #define RM_CAP_I1 64
 #endif
@@ -169,7 +172,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       // the segment end as its scalar bound.  Between segments a lane's exit test
       // is re-formed from its last (t, dl) (same operations, same result), the
       // lanes still marching take the check, and those that go on take the step.
-      int ib = i0, iend = RM_CAP_EXIT ? RM_CAP_I0 : nmax;
+      int ib = i0, iend = (RM_CAP_EXIT && (RM_CAP_REFL || !reflected)) ? RM_CAP_I0 : nmax;
       bool live = true;
 #pragma unroll 1
       for (;;) {
