@@ -136,9 +136,17 @@ def main() -> int:
             print("bench.py: --gpus N > 1 must be launched with torch.distributed.run",
                   file=sys.stderr)
             return 2
+    # Rehearsal knobs (tests/test_gpu_bench_dist.py, one GPU): RM_BENCH_DEVICE puts every
+    # rank on one device, RM_BENCH_BACKEND=gloo gathers through host memory.  The
+    # driver's multi-GPU runs use neither: one rank per GPU, RCCL ("nccl").
+    backend = os.environ.get("RM_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("RM_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     cfg = CONFIGS[args.config]
     W, H = cfg["width"], cfg["height"]
@@ -197,15 +205,24 @@ def main() -> int:
         else:
             rs[j].dispatch(uniforms(f))
 
+    def gather(src):
+        if backend == "nccl":
+            dist.gather(src, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            return
+        host = src.cpu()  # gloo rehearsal: host staging (synchronous on the current stream)
+        hl = [torch.empty_like(host) for _ in range(ws)] if rank == 0 else None
+        dist.gather(host, gather_list=hl, dst=0)
+        if rank == 0:
+            gathered.copy_(torch.stack(hl).to(gathered.device))
+
     def step(f):
         j = f % nfl
         if ws == 1:
             render(j, f)
             return
-        glist = list(gathered.unbind(0)) if rank == 0 else None
         if not args.pipeline:
             render(0, f)
-            dist.gather(outs[0], gather_list=glist, dst=0)
+            gather(outs[0])
             if rank == 0:
                 ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
             return
@@ -216,7 +233,7 @@ def main() -> int:
         render_done[j].record(streams[j])
         with torch.cuda.stream(comm):
             comm.wait_event(render_done[j])
-            dist.gather(outs[j], gather_list=glist, dst=0)
+            gather(outs[j])
             if rank == 0:
                 ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
             gather_done[j].record(comm)
@@ -265,7 +282,7 @@ def main() -> int:
                              "(the timed region overlaps frames)")
     elapsed = t1 - t0
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     frames = args.steps
@@ -322,6 +339,18 @@ def main() -> int:
         d = np.abs(g.astype(np.int16) - ref["rgba8"].astype(np.int16))
         parity = {"max_abs_delta_rgba8": int(d.max()), "pixels_over_2": int((d.max(-1) > 2).sum()),
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
+
+    # ---- N > 1: the assembled frame of the last step against a single-GPU render ----
+    if ws > 1 and rank == 0:
+        torch.cuda.synchronize()
+        last = args.warmup + args.steps - 1
+        with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local) as rf:
+            rf.dispatch(uniforms(last))
+            full = rf.read_rgba8()
+        d = np.abs(frame.cpu().numpy().astype(np.int16) - full.astype(np.int16))
+        parity = {"assembled_equals_single_gpu": bool(d.max() == 0),
+                  "max_abs_delta_rgba8": int(d.max()), "pixels_checked": int(W * H),
+                  "reference": f"single-GPU render of sweep frame {last % SWEEP_FRAMES}"}
 
     if rank == 0:
         out = {
