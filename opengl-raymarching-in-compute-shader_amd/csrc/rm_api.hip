@@ -614,13 +614,13 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
     c->scene.clear();
     return RM_OK;
   }
-  std::vector<uint32_t> words((size_t)(n > 0 ? n : 0) * rm::TABLE_WORDS);
+  std::vector<uint32_t> words(rm::scene_words(n > 0 && n <= RM_MAX_PRIMITIVES ? n : 0));
   const char* why = "rm_set_scene: bad table";
   if (rm::compile_scene(prims, n, words.data(), &why) != RM_OK) return fail(c, RM_ERR_INVALID, why);
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   if (!c->d_scene) {
-    RM_HIP(c, hipMalloc(&c->d_scene, (size_t)RM_MAX_PRIMITIVES * rm::TABLE_WORDS * sizeof(uint32_t)));
+    RM_HIP(c, hipMalloc(&c->d_scene, rm::scene_words(RM_MAX_PRIMITIVES) * sizeof(uint32_t)));
   }
   // Ordered on the context's stream after the frames already queued (they keep
   // reading the previous table); the host copy must outlive the async copy, so

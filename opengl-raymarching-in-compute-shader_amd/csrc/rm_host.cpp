@@ -12,6 +12,8 @@
 #include <cmath>
 #include <cstring>
 #include <initializer_list>
+#include <limits>
+#include <vector>
 
 #include "rm_internal.hpp"
 
@@ -418,6 +420,123 @@ extern "C" int rm_default_scene(rm_primitive* out, int32_t capacity, int32_t* n)
 
 namespace rm {
 
+// Exit header of a table (rm_internal.hpp ExitWord; used by rm_table.hip).  In
+// exact arithmetic every entry's distance is bounded below by a ball or is
+// linear:
+//   sphere  |q| - r;  box (a >= 0)  >= |q| - |a|;  blend (a >= 0, weights in
+//   [0, 1])  >= |q| - max(|a|, r);  torus  >= |q| - (|R| + r) (triangle
+//   inequality);  capsule  >= |q - M| - (|ba|/2 + r), M = a + ba/2;
+//   plane  = dot(q, n) + w, linear along a ray;
+// q = swizzle(p - c) is an isometry of p - c, so the balls map back to world
+// space.  C is the mean of the ball centres and R >= max_k(|C - c_k| + R_k),
+// rounded up.  The float error of an entry's value at p is below
+// 40 u N (|p|_1 + S_k) (u = 2^-24; S_k = |c_k|_1 + sum |params|; N = the largest
+// plane |n|_1, >= 1); the device slack sigma (|p|_1 + S), sigma = 2^-12 N,
+// S = max_k S_k + 1, is two orders of magnitude above it.
+// The same balls serve the per-point culling of the table kernels' sdf (word
+// TW_BALL of each entry; spheres and planes, whose exact values cost no more
+// than a bound, and every entry of a table without valid bounds get +inf).
+static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
+  uint32_t* hdr = out + (size_t)n * TABLE_WORDS;
+  float h[EXIT_WORDS];
+  std::memset(h, 0, sizeof h);
+  std::vector<double> cx, cy, cz, rr;
+  std::vector<int32_t> ball_of;  // entry of each ball
+  double S = 0.0, N = 1.0;
+  int np = 0;
+  bool ok = true;
+  for (int32_t k = 0; k < n && ok; ++k) {
+    const rm_primitive& p = prims[k];
+    double a[7];
+    for (int j = 0; j < 7; ++j) a[j] = p.param[j];
+    double sk = std::fabs((double)p.center[0]) + std::fabs((double)p.center[1]) + std::fabs((double)p.center[2]);
+    for (int j = 0; j < 7; ++j) sk += std::fabs(a[j]);
+    if (!std::isfinite(sk)) ok = false;
+    S = std::max(S, sk);
+    // world offset of a q-space vector (the swizzle is its own inverse)
+    auto world = [&](double x, double y, double z, double* o) {
+      o[0] = x;
+      o[1] = p.swizzle == RM_SWIZZLE_XZY ? z : y;
+      o[2] = p.swizzle == RM_SWIZZLE_XZY ? y : z;
+    };
+    double m[3] = {0.0, 0.0, 0.0}, R = 0.0;
+    switch (p.type) {
+      case RM_PRIM_SPHERE: R = a[0]; break;
+      case RM_PRIM_BOX:
+      case RM_PRIM_BLEND:
+        if (a[0] < 0.0 || a[1] < 0.0 || a[2] < 0.0) ok = false;
+        R = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (p.type == RM_PRIM_BLEND) R = std::max(R, a[3]);
+        break;
+      case RM_PRIM_TORUS: R = std::fabs(a[0]) + a[1]; break;
+      case RM_PRIM_CAPSULE: {
+        const double bx = a[3] - a[0], by = a[4] - a[1], bz = a[5] - a[2];
+        const double bl = std::sqrt(bx * bx + by * by + bz * bz);
+        // the kernel divides by the float dot(ba, ba); 0 gives NaN distances
+        const float fbx = p.param[3] - p.param[0], fby = p.param[4] - p.param[1], fbz = p.param[5] - p.param[2];
+        if (!((fbx * fbx + fby * fby) + fbz * fbz > 0.0f)) ok = false;
+        world(a[0] + bx / 2, a[1] + by / 2, a[2] + bz / 2, m);
+        R = bl / 2 + a[6];
+        break;
+      }
+      default: {  // plane
+        if (np == EX_MAX_PLANES) {
+          ok = false;
+          break;
+        }
+        double nw[3];
+        world(a[0], a[1], a[2], nw);
+        const double off = a[3] - (nw[0] * p.center[0] + nw[1] * p.center[1] + nw[2] * p.center[2]);
+        float* pl = h + EX_PLANES + 4 * np++;
+        for (int j = 0; j < 3; ++j) pl[j] = (float)nw[j];
+        pl[3] = (float)off;
+        N = std::max(N, std::fabs(nw[0]) + std::fabs(nw[1]) + std::fabs(nw[2]));
+        continue;
+      }
+    }
+    cx.push_back(p.center[0] + m[0]);
+    cy.push_back(p.center[1] + m[1]);
+    cz.push_back(p.center[2] + m[2]);
+    rr.push_back(R);
+    ball_of.push_back(k);
+  }
+  double C[3] = {0.0, 0.0, 0.0}, RA = 0.0;
+  if (!cx.empty()) {
+    for (size_t k = 0; k < cx.size(); ++k) C[0] += cx[k], C[1] += cy[k], C[2] += cz[k];
+    for (double& v : C) v = (double)(float)(v / (double)cx.size());  // the device's float centre
+    for (size_t k = 0; k < cx.size(); ++k) {
+      const double dx = cx[k] - C[0], dy = cy[k] - C[1], dz = cz[k] - C[2];
+      RA = std::max(RA, std::sqrt(dx * dx + dy * dy + dz * dz) + rr[k]);
+    }
+  } else {
+    RA = -1e30;  // no bounded entry: the ball bound never binds
+  }
+  const double sigma = 0x1p-12 * N;
+  ok = ok && std::isfinite(RA) && std::isfinite(S) && std::isfinite(sigma) && S < 1e15;
+  h[EX_VALID] = ok ? 1.0f : 0.0f;
+  h[EX_CX] = (float)C[0], h[EX_CY] = (float)C[1], h[EX_CZ] = (float)C[2];
+  h[EX_R] = (float)(RA * (1.0 + 0x1p-20) + 0x1p-20 * (1.0 + std::fabs(RA)));  // rounded up
+  h[EX_SIGMA] = (float)(sigma * (1.0 + 0x1p-20));
+  h[EX_S] = (float)((S + 1.0) * (1.0 + 0x1p-20));
+  h[EX_NPLANES] = (float)np;
+  std::memcpy(hdr, h, sizeof h);
+  const float INF = std::numeric_limits<float>::infinity();
+  for (int32_t k = 0; k < n; ++k) {
+    float b[4] = {0.0f, 0.0f, 0.0f, INF};
+    std::memcpy(out + (size_t)k * TABLE_WORDS + TW_BALL, b, sizeof b);
+  }
+  if (!ok) return;
+  for (size_t j = 0; j < ball_of.size(); ++j) {
+    if (prims[ball_of[j]].type == RM_PRIM_SPHERE) continue;
+    // centre rounded to float; the radius absorbs that rounding and is rounded up
+    const float c[3] = {(float)cx[j], (float)cy[j], (float)cz[j]};
+    const double e = std::fabs(c[0] - cx[j]) + std::fabs(c[1] - cy[j]) + std::fabs(c[2] - cz[j]);
+    const float b[4] = {c[0], c[1], c[2],
+                        (float)((rr[j] + e) * (1.0 + 0x1p-20) + 0x1p-20 * (1.0 + std::fabs(rr[j])))};
+    std::memcpy(out + (size_t)ball_of[j] * TABLE_WORDS + TW_BALL, b, sizeof b);
+  }
+}
+
 int compile_scene(const rm_primitive* prims, int32_t n, uint32_t* out, const char** why) {
   auto bad = [&](const char* m) {
     if (why) *why = m;
@@ -458,6 +577,7 @@ int compile_scene(const rm_primitive* prims, int32_t n, uint32_t* out, const cha
     w[TW_ID] = (uint32_t)p.id;
     w[TW_PAINT] = (uint32_t)p.paint;
   }
+  exit_bounds(prims, n, out);
   return RM_OK;
 }
 

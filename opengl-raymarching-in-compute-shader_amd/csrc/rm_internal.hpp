@@ -18,12 +18,26 @@ int32_t* uniform_ints(rm_uniforms* u, const char* name);
 // floats: material, colour[3], centre[3], then the per-type parameters with
 // the uniform-only subexpressions folded in on the host (capsule ba = b - a,
 // dot(ba, ba): the same float operations the GLSL performs per call).
-constexpr int TABLE_WORDS = 20;
+constexpr int TABLE_WORDS = 24;
 enum TableWord : int {
   TW_TYPE = 0, TW_SWIZZLE = 1, TW_ID = 2, TW_PAINT = 3, TW_MATERIAL = 4, TW_COLOR = 5,
   TW_CENTER = 8, TW_P = 11,  // 9 parameter words
+  TW_BALL = 20,              // culling ball: world centre (3), radius (+inf: never culled)
 };
-// Validates prims[0..n) and writes n * TABLE_WORDS words to out; returns
+// After the n entries: EXIT_WORDS words of per-table bounds for the provable
+// early exits of the table kernels (rm_table.hip): every non-plane entry lies in
+// the ball (EX_C, EX_R); planes are linear along a ray; EX_SIGMA, EX_S scale the
+// float-error slack.  EX_VALID = 0 disables the exits (unbounded or degenerate
+// entries, more than EX_MAX_PLANES planes).
+constexpr int EX_MAX_PLANES = 4;
+constexpr int EXIT_WORDS = 8 + 4 * EX_MAX_PLANES;
+enum ExitWord : int {
+  EX_VALID = 0, EX_CX = 1, EX_CY = 2, EX_CZ = 3, EX_R = 4, EX_SIGMA = 5, EX_S = 6,
+  EX_NPLANES = 7, EX_PLANES = 8,  // per plane: world normal n' (3), offset: value ~ dot(p, n') + off
+};
+// Words for n entries plus the exit header.
+constexpr size_t scene_words(int n) { return (size_t)n * TABLE_WORDS + EXIT_WORDS; }
+// Validates prims[0..n) and writes scene_words(n) words to out; returns
 // RM_OK or RM_ERR_INVALID with *why set.
 int compile_scene(const rm_primitive* prims, int32_t n, uint32_t* out, const char** why);
 

@@ -44,6 +44,12 @@
 #define RM_CAP_I1 64
 #endif
 
+#ifndef RM_STEP_UNROLL
+#define RM_STEP_UNROLL 1
+#endif
+#define RM_STR_(x) #x
+#define RM_UNROLL(n) _Pragma(RM_STR_(unroll n))
+
 namespace rmd {
 
 #ifdef RM_WAVE_TIMES
@@ -177,6 +183,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll 1
       for (;;) {
         if (live) {
+          RM_UNROLL(RM_STEP_UNROLL)
           for (int i = ib;; ++i) {
             const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
             const bool h = d < 0.000001f * t;

@@ -39,6 +39,9 @@ struct TCnt {
 
 using rm::TABLE_WORDS;
 
+#ifndef RM_TABLE_CULL
+#define RM_TABLE_CULL 1
+#endif
 #ifndef RM_TABLE_FAST_SQRT
 #define RM_TABLE_FAST_SQRT 0
 #endif
@@ -91,16 +94,46 @@ struct Table {
   int n;
   float blend, omblend;
 
+  __device__ __forceinline__ const float* exits() const { return t + n * TABLE_WORDS; }
+
   __device__ __forceinline__ const float* entry(int k) const { return t + k * TABLE_WORDS; }
   __device__ __forceinline__ int type(int k) const {
     return __builtin_amdgcn_readfirstlane(__float_as_int(entry(k)[rm::TW_TYPE]));
   }
-  // sdf(p).hitpoint and the index of the opU winner
+  // sdf(p).hitpoint and the index of the opU winner.
+  //
+  // Culling (RM_TABLE_CULL): an entry whose lower bound at p exceeds an upper
+  // bound U of the final minimum is strictly above that minimum, so it can
+  // neither be the opU winner nor tie it (ties go to the later entry) and
+  // skipping it leaves (d, best) unchanged.  U = min(running minimum, the
+  // planes' values at p computed first with the same operations); the bound
+  // is |p - c'| - R - slack(p) from the entry's ball (TW_BALL, rm::exit_bounds),
+  // slack(p) = sigma (|p|_1 + S) (rounded up) covering the float error of the
+  // entry's value and of the bound.  A culled entry's value is finite (its
+  // |p - c'| < 2^60, finite parameters), so NaN propagation through opU is
+  // unchanged too.  d starts at +inf: opU(+inf, v) takes v for every v, as the
+  // GLSL's first assignment does.
   __device__ __forceinline__ float dist(f3 p, int& best) const {
-    float d = prim_dist(entry(0), type(0), p, blend, omblend);
+    const float INF = __builtin_huge_valf();
+    float U = INF, slack = 0.0f;
+    if (RM_TABLE_CULL) {
+      for (int k = 0; k < n; ++k)
+        if (type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(entry(k), RM_PRIM_PLANE, p, blend, omblend));
+      const float* ex = exits();
+      slack = ex[rm::EX_SIGMA] * (((fabsf(p.x) + fabsf(p.y)) + fabsf(p.z)) + ex[rm::EX_S]) *
+              ((1.0f + 0x1p-12f) * (1.0f + 0x1p-12f));
+    }
+    float d = INF;
     best = 0;
-    for (int k = 1; k < n; ++k) {
-      const float dk = prim_dist(entry(k), type(k), p, blend, omblend);
+    for (int k = 0; k < n; ++k) {
+      const float* P = entry(k);
+      if (RM_TABLE_CULL && P[rm::TW_BALL + 3] != INF) {
+        const float bx = p.x - P[rm::TW_BALL], by = p.y - P[rm::TW_BALL + 1], bz = p.z - P[rm::TW_BALL + 2];
+        const float x = (bx * bx + by * by) + bz * bz;
+        const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), 1.0f - 0x1p-12f, -(P[rm::TW_BALL + 3] + slack));
+        if ((lb > gmin(d, U)) & (x < 0x1p120f)) continue;
+      }
+      const float dk = prim_dist(P, type(k), p, blend, omblend);
       const bool keep = d < dk;  // opU(t, new) = (t < new) ? t : new
       best = keep ? best : k;
       d = keep ? d : dk;
@@ -119,6 +152,57 @@ struct Table {
   __device__ __forceinline__ float material(int k) const { return entry(k)[rm::TW_MATERIAL]; }
 };
 
+#ifndef RM_TABLE_EXITS
+#define RM_TABLE_EXITS 1
+#endif
+// Provable early exits for any table (the generic form of rm_scene.hpp's
+// lin_exit_T; bounds from rm::exit_bounds, rm_host.cpp).  Every entry's float
+// value at p(t) = ro + rd t is at least
+//   |rd| t - |ro - C| - R - slack(t)            (entries inside the ball C, R)
+//   dot(ro, n') + off + dot(rd, n') t - slack(t) (plane entries)
+// with slack(t) = s0 + s1 t = sigma (|ro|_1 + S) + sigma |rd|_1 t (rounded up),
+// all linear in t.  Once each bound stays above max(hmin, c t) for every later
+// t -- past T, returned here (+inf: not provable) -- no later step of a march
+// along the ray can see a distance <= hmin or a ratio d / t <= c:
+//   * RayMarch / reflectedRay: c = 1e-6 (1 + 2^-9), hmin = 0: no later step
+//     hits, the march ends in a miss (t is discarded);
+//   * softshadow (rd = light - pos): c = (1 + 2^-9) / k, hmin = 0.001: no
+//     later step returns 0.05 and every k h / t rounds above 1 >= res.
+// Coefficients are rounded toward failure (2^-12 relative, 2^-20 absolute terms),
+// as in lin_exit_T.
+__device__ __forceinline__ float table_exit_T(const float* ex, float c, float hmin, f3 ro, f3 rd) {
+  const float INF = __builtin_huge_valf();
+  if (!RM_TABLE_EXITS || ex[rm::EX_VALID] == 0.0f) return INF;
+  const float HI = 1.0f + 0x1p-12f, LO = 1.0f - 0x1p-12f;
+  const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
+  const float sig = ex[rm::EX_SIGMA];
+  const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
+  const float rd1 = (fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z);
+  const float s0 = sig * (ro1 + ex[rm::EX_S]) * (HI * HI);
+  const float s1 = sig * rd1 * (HI * HI);
+  float T = -INF;
+  if (ex[rm::EX_R] > -1e29f) {  // the ball of the bounded entries
+    const float ex0 = ro.x - ex[rm::EX_CX], ey = ro.y - ex[rm::EX_CY], ez = ro.z - ex[rm::EX_CZ];
+    const float rc = __builtin_fmaf(__builtin_amdgcn_sqrtf((ex0 * ex0 + ey * ey) + ez * ez), HI, 0x1p-18f);
+    const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd));
+    const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
+    const float b1 = (rc + ex[rm::EX_R] + s0 + hmin) * HI;
+    if (!(a1 > 0.0f)) return INF;
+    T = b1 * __builtin_amdgcn_rcpf(a1) * UP;
+  }
+  const int np = (int)ex[rm::EX_NPLANES];
+  for (int j = 0; j < np; ++j) {
+    const float* pl = ex + rm::EX_PLANES + 4 * j;
+    const f3 nw = mk(pl[0], pl[1], pl[2]);
+    const float A = dot(ro, nw) + pl[3], B = dot(rd, nw);
+    const float a2 = (B - s1 - c) - 0x1p-20f * (fabsf(B) + s1 + c);
+    const float b2 = (A - s0 - hmin) - 0x1p-20f * (fabsf(A) + s0 + hmin);
+    if (!(a2 > 0.0f)) return INF;
+    T = __builtin_fmaxf(T, -(b2 * __builtin_amdgcn_rcpf(a2) * (b2 >= 0.0f ? DN : UP)));
+  }
+  return T;
+}
+
 struct THit {
   float t;  // -1: the dummy RayHit {-1, 0, -1, 1.0} (glsl:128)
   int id;
@@ -132,7 +216,15 @@ __device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   float t = 0.0f;
+  // provable miss (table_exit_T): production stops there; the counting build
+  // runs on and poisons the colour with NaN should the ray hit after all
+  const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
+  bool proven = false;
   for (int i = 0; i < nmax; ++i) {
+    if (t > T) {
+      if (!COUNT) break;
+      proven = true;
+    }
     const f3 p = add(ro, muls(rd, t));
     int k;
     const float d = S.dist(p, k);
@@ -140,7 +232,9 @@ __device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
       if (reflected) c.reflect++;
       else c.march++;
     }
-    if (d < 0.000001f * t) return THit{t, S.id(k), S.material(k), S.color(k, p)};
+    if (d < 0.000001f * t)
+      return THit{t, S.id(k), S.material(k),
+                  (COUNT && proven) ? mk(__builtin_nanf(""), 0.0f, 0.0f) : S.color(k, p)};
     if (d > tmax) break;
     t += d;
   }
@@ -163,7 +257,13 @@ __device__ f3 tnormal(const Table& S, f3 pos, TCnt& c) {
 template <bool COUNT>
 __device__ float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   float res = 1.0f, t = 0.0f;
+  const float c_sh = (F.k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / F.k * (1.0f + 0x1p-12f);
+  const float T = table_exit_T(S.exits(), c_sh, 0.001f, ro, rd);
   for (int i = 0; i < 16; ++i) {
+    if (t > T) {  // the remaining steps are no-ops (table_exit_T)
+      if (COUNT) c.shadow += 16 - i;
+      return res;
+    }
     int k;
     const float h = S.dist(add(ro, muls(rd, t)), k);
     if (COUNT) c.shadow++;
@@ -233,7 +333,7 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   S.blend = F.blend;
   S.omblend = F.omblend;
   if (RM_TABLE_LDS) {
-    for (int i = threadIdx.x; i < F.nprims * TABLE_WORDS; i += blockDim.x) lds[i] = F.scene[i];
+    for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
     __syncthreads();
     S.t = lds;
   } else {
@@ -328,7 +428,7 @@ __global__ __launch_bounds__(64) void k_table_sample(Frame F) {
 namespace rm {
 
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s) {
-  const size_t lds = RM_TABLE_LDS ? (size_t)F.nprims * TABLE_WORDS * sizeof(float) : 0;
+  const size_t lds = RM_TABLE_LDS ? rm::scene_words(F.nprims) * sizeof(float) : 0;
   if (F.aa) {
     const dim3 g((F.width + 3) / 4, (F.rows + 3) / 4);
     if (counters)

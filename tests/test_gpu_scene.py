@@ -59,12 +59,16 @@ def test_default_table_equals_builtin_kernel_full_hd(rm, gpu):
     np.testing.assert_array_equal(got["rgba32f"], ref["rgba32f"])
 
 
-def random_scene(rm, seed):
+def random_scene(rm, seed, nplanes=None):
+    """Random table; nplanes fixes the number of plane entries (None: random types)."""
     g = np.random.default_rng(seed)
     n = int(g.integers(3, 13))
+    types = [int(g.integers(0, 6)) for _ in range(n)]
+    if nplanes is not None:
+        types = [int(g.integers(0, 5)) for _ in range(n)] + [rm.PRIM_PLANE] * nplanes
+        g.shuffle(types)
     prims = []
-    for k in range(n):
-        t = int(g.integers(0, 6))
+    for t in types:
         c = (float(g.uniform(-18, 18)), float(g.uniform(-3, 3)), float(g.uniform(-35, 0)))
         if t == rm.PRIM_SPHERE:
             par = (float(g.uniform(0.5, 4)),)
@@ -79,6 +83,8 @@ def random_scene(rm, seed):
         else:
             nv = g.normal(size=3)
             nv[1] = abs(nv[1]) + 1.0
+            if nplanes is not None and g.uniform() < 0.5:
+                nv[1] = -nv[1]  # a ceiling: rays going up meet it, the miss exit must not fire
             nv /= np.linalg.norm(nv)
             c = (0.0, 0.0, 0.0)
             par = (float(nv[0]), float(nv[1]), float(nv[2]), float(g.uniform(4, 7)))
@@ -181,3 +187,21 @@ def test_table_shards_assemble(rm, gpu):
             if g >= 0:
                 got[g] = parts[s][lr]
     np.testing.assert_array_equal(got, full)
+
+
+# The table kernels' provable early exits (rm_table.hip table_exit_T) on tables
+# without a plane (sky rays leave through the ball bound alone), with several
+# floor / ceiling planes, and with more planes than the exit header holds (exits
+# off).  The counting build runs every step and poisons a proven miss that hits
+# (NaN), so the counts, images and NaN masks check the proofs.
+@pytest.mark.parametrize("seed,nplanes", [(100, 0), (101, 0), (102, 2), (103, 3), (104, 1), (105, 5)])
+def test_table_exits_match_oracle(rm, oracle, gpu, seed, nplanes):
+    scene = random_scene(rm, seed, nplanes=nplanes)
+    f, b, aa, sm = [(20, 3, True, 0), (70, 2, False, 0), (110, 4, True, 1)][seed % 3]
+    u = rm.sweep_uniforms(f, 120, b, aa, sm)
+    W, H = 96, 64
+    ref = oracle.render(u, W, H, scene=scene)
+    got = _render(rm, u, W, H, scene=scene)
+    _compare(ref, got, f"seed {seed}")
+    prod = _render(rm, u, W, H, scene=scene, counters=False)
+    np.testing.assert_array_equal(prod["rgba32f"], got["rgba32f"])
