@@ -48,7 +48,8 @@ def main(src, tag, workload="cfg3", dst="profiles"):
             cs["hbm_bytes_per_launch"] = 2 * f + w
     # bench.py matches a summary to its workload through _meta
     out["_meta"] = {"workload": workload, "source": os.path.basename(os.path.normpath(src)),
-                    "passes": "separate rocprofv3 --pmc runs of tools/prof_kernels.py pixel 3 3"}
+                    "passes": "separate rocprofv3 --pmc runs of tools/prof_kernels.py "
+                              + os.environ.get("PROF_KIND", "pixel") + " 3 3"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     log = open(os.path.join(src, "bench_traced.log")).read().splitlines()
     line = [l for l in log if l.startswith("{")]
