@@ -433,16 +433,15 @@ namespace rm {
 // 40 u N (|p|_1 + S_k) (u = 2^-24; S_k = |c_k|_1 + sum |params|; N = the largest
 // plane |n|_1, >= 1); the device slack sigma (|p|_1 + S), sigma = 2^-12 N,
 // S = max_k S_k + 1, is two orders of magnitude above it.
-// The same balls serve the per-point culling of the table kernels' sdf (word
-// TW_BALL of each entry; spheres and planes, whose exact values cost no more
-// than a bound, and every entry of a table without valid bounds get +inf).
+// The same balls serve the culling of the table kernels' sdf (word TW_BALL of
+// each entry; planes and every entry of a table without valid bounds get +inf).
 static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
   uint32_t* hdr = out + (size_t)n * TABLE_WORDS;
   float h[EXIT_WORDS];
   std::memset(h, 0, sizeof h);
   std::vector<double> cx, cy, cz, rr;
   std::vector<int32_t> ball_of;  // entry of each ball
-  double S = 0.0, N = 1.0;
+  double S = 0.0, N = 1.0, lip = 1.0;
   int np = 0;
   bool ok = true;
   for (int32_t k = 0; k < n && ok; ++k) {
@@ -491,6 +490,7 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
         for (int j = 0; j < 3; ++j) pl[j] = (float)nw[j];
         pl[3] = (float)off;
         N = std::max(N, std::fabs(nw[0]) + std::fabs(nw[1]) + std::fabs(nw[2]));
+        lip = std::max(lip, std::sqrt(nw[0] * nw[0] + nw[1] * nw[1] + nw[2] * nw[2]));
         continue;
       }
     }
@@ -519,6 +519,19 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
   h[EX_SIGMA] = (float)(sigma * (1.0 + 0x1p-20));
   h[EX_S] = (float)((S + 1.0) * (1.0 + 0x1p-20));
   h[EX_NPLANES] = (float)np;
+  h[EX_LIP] = (float)(lip * (1.0 + 0x1p-20));
+  uint32_t eval_mask = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+  int ns = 0;
+  for (size_t j = 0; ok && j < ball_of.size() && ns < EX_MAX_SLOTS; ++j) {
+    h[EX_SLOTS + ns++] = (float)ball_of[j];
+    eval_mask &= ~(1u << ball_of[j]);
+  }
+  h[EX_NSLOTS] = (float)ns;
+  std::memcpy(&h[EX_EVAL_MASK], &eval_mask, sizeof eval_mask);
+  uint32_t plane_mask = 0;
+  for (int32_t k = 0; k < n; ++k)
+    if (prims[k].type == RM_PRIM_PLANE) plane_mask |= 1u << k;
+  std::memcpy(&h[EX_PLANE_MASK], &plane_mask, sizeof plane_mask);
   std::memcpy(hdr, h, sizeof h);
   const float INF = std::numeric_limits<float>::infinity();
   for (int32_t k = 0; k < n; ++k) {
@@ -527,7 +540,6 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
   }
   if (!ok) return;
   for (size_t j = 0; j < ball_of.size(); ++j) {
-    if (prims[ball_of[j]].type == RM_PRIM_SPHERE) continue;
     // centre rounded to float; the radius absorbs that rounding and is rounded up
     const float c[3] = {(float)cx[j], (float)cy[j], (float)cz[j]};
     const double e = std::fabs(c[0] - cx[j]) + std::fabs(c[1] - cy[j]) + std::fabs(c[2] - cz[j]);

@@ -29,12 +29,20 @@ enum TableWord : int {
 // the ball (EX_C, EX_R); planes are linear along a ray; EX_SIGMA, EX_S scale the
 // float-error slack.  EX_VALID = 0 disables the exits (unbounded or degenerate
 // entries, more than EX_MAX_PLANES planes).
+// The same header lists the entries the march tracks lazily (EX_SLOTS, at most
+// EX_MAX_SLOTS bounded entries, in table order), the bitmask of the entries
+// evaluated at every step (EX_EVAL_MASK, bit k = entry k: planes and untracked
+// entries), and EX_LIP >= 1, a Lipschitz constant of the scene minimum (the
+// largest plane |n|; every other entry is 1-Lipschitz).
 constexpr int EX_MAX_PLANES = 4;
-constexpr int EXIT_WORDS = 8 + 4 * EX_MAX_PLANES;
+constexpr int EX_MAX_SLOTS = 8;
 enum ExitWord : int {
   EX_VALID = 0, EX_CX = 1, EX_CY = 2, EX_CZ = 3, EX_R = 4, EX_SIGMA = 5, EX_S = 6,
   EX_NPLANES = 7, EX_PLANES = 8,  // per plane: world normal n' (3), offset: value ~ dot(p, n') + off
+  EX_LIP = EX_PLANES + 4 * EX_MAX_PLANES, EX_NSLOTS, EX_EVAL_MASK, EX_PLANE_MASK, EX_SLOTS,
+  EX_END = EX_SLOTS + EX_MAX_SLOTS,
 };
+constexpr int EXIT_WORDS = EX_END;
 // Words for n entries plus the exit header.
 constexpr size_t scene_words(int n) { return (size_t)n * TABLE_WORDS + EXIT_WORDS; }
 // Validates prims[0..n) and writes scene_words(n) words to out; returns

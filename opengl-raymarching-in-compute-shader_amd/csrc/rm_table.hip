@@ -42,6 +42,9 @@ using rm::TABLE_WORDS;
 #ifndef RM_TABLE_CULL
 #define RM_TABLE_CULL 1
 #endif
+#ifndef RM_TABLE_LAZY
+#define RM_TABLE_LAZY 1
+#endif
 #ifndef RM_TABLE_FAST_SQRT
 #define RM_TABLE_FAST_SQRT 0
 #endif
@@ -127,7 +130,8 @@ struct Table {
     best = 0;
     for (int k = 0; k < n; ++k) {
       const float* P = entry(k);
-      if (RM_TABLE_CULL && P[rm::TW_BALL + 3] != INF) {
+      // (spheres: the exact value costs no more than the bound)
+      if (RM_TABLE_CULL && P[rm::TW_BALL + 3] != INF && type(k) != RM_PRIM_SPHERE) {
         const float bx = p.x - P[rm::TW_BALL], by = p.y - P[rm::TW_BALL + 1], bz = p.z - P[rm::TW_BALL + 2];
         const float x = (bx * bx + by * by) + bz * bz;
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), 1.0f - 0x1p-12f, -(P[rm::TW_BALL + 3] + slack));
@@ -135,6 +139,22 @@ struct Table {
       }
       const float dk = prim_dist(P, type(k), p, blend, omblend);
       const bool keep = d < dk;  // opU(t, new) = (t < new) ? t : new
+      best = keep ? best : k;
+      d = keep ? d : dk;
+    }
+    return d;
+  }
+  // sdf(p) over the entries whose bit is set in `mask` (the others are proven
+  // strictly above the minimum by the march's lazy culling), opU in table order
+  // `wave` (uniform) has every bit some lane of the wave has in `mask`.
+  __device__ __forceinline__ float dist_mask(f3 p, uint32_t mask, uint32_t wave, int& best) const {
+    float d = __builtin_huge_valf();
+    best = 0;
+    for (; wave; wave &= wave - 1u) {
+      const int k = __builtin_ctz(wave);
+      if (!((mask >> k) & 1u)) continue;
+      const float dk = prim_dist(entry(k), type(k), p, blend, omblend);
+      const bool keep = d < dk;
       best = keep ? best : k;
       d = keep ? d : dk;
     }
@@ -220,14 +240,72 @@ __device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
   // runs on and poisons the colour with NaN should the ray hit after all
   const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
   bool proven = false;
+  // Lazy culling along the ray (RM_TABLE_LAZY; the generic form of scene_lazy,
+  // rm_scene.hpp): slot j tracks entry k_j (rm::exit_bounds) with an expiry
+  // te[j] before which k_j is proven strictly above the minimum.  A re-test at
+  // p = p(t) bounds k_j below by its ball, lb = |p - c'| - R, and the minimum
+  // above by U = min(the planes' values at p, d_prev (1 + L |rd|) + sl): the
+  // previous step moved p by |rd| d_prev and the minimum is L-Lipschitz.  With
+  // sl = 2 sigma (|p|_1 + |ro|_1 + S) covering the float error of both sides
+  // (and of p(t) itself), k_j stays above the minimum while
+  // t' - t < g / ((1 + L) |rd| + 2 sigma |rd|_1), g = lb - U - sl (the second
+  // term: the slack's growth along the ray); g <= 0 evaluates k_j now.  Untracked entries and planes are evaluated at every
+  // step (EX_EVAL_MASK).  Lanes whose te has not expired re-test for free and
+  // keep the later expiry.  The negated compares send NaN rays (degenerate
+  // uniforms) through the re-test, whose NaN bound evaluates every entry.
+  constexpr int KL = rm::EX_MAX_SLOTS;
+  const float* ex = S.exits();
+  const int ns = RM_TABLE_LAZY ? (int)ex[rm::EX_NSLOTS] : 0;
+  const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
+  const uint32_t always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
+  const float INF = __builtin_huge_valf();
+  float te[KL];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) te[j] = j < ns ? -INF : INF;
+  float temin = ns > 0 ? -INF : INF;
+  const float lip = ex[rm::EX_LIP], sig2 = 2.0f * ex[rm::EX_SIGMA];
+  const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+  const float rd1 = ((fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z)) * (1.0f + 0x1p-16f);
+  const float sl0 = (((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z)) + ex[rm::EX_S]) * (1.0f + 0x1p-16f);
+  // the slack grows by sig2 |rd|_1 per unit of t
+  const float inv = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf((1.0f + lip) * rdl + sig2 * rd1) * (1.0f - 0x1p-16f);
+  const float grow = (__builtin_fmaf(lip, rdl, 1.0f) + sig2 * rd1) * (1.0f + 0x1p-10f);
+  float dprev = INF;
   for (int i = 0; i < nmax; ++i) {
     if (t > T) {
       if (!COUNT) break;
       proven = true;
     }
     const f3 p = add(ro, muls(rd, t));
+    uint32_t mask = always, wmask = always;
+    if (ns > 0 && __any(!(t < temin))) {
+      const float sl = sig2 * (((fabsf(p.x) + fabsf(p.y)) + fabsf(p.z)) + sl0) * (1.0f + 0x1p-10f);
+      float U = __builtin_fmaf(dprev, grow, sl);
+      for (uint32_t pm = __float_as_uint(ex[rm::EX_PLANE_MASK]); pm; pm &= pm - 1u)
+        U = gmin(U, prim_dist(S.entry(__builtin_ctz(pm)), RM_PRIM_PLANE, p, S.blend, S.omblend));
+#pragma unroll
+      for (int j = 0; j < KL; ++j) {
+        if (j < ns && __any(!(t < te[j]))) {
+          const int k = (int)ex[rm::EX_SLOTS + j];
+          const float* B = S.entry(k) + rm::TW_BALL;
+          const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
+          const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
+                                          1.0f - 0x1p-12f, -B[3]);
+          const float g = lb - U - sl;
+          const bool expired = !(t < te[j]);
+          te[j] = __builtin_fmaxf(te[j], __builtin_fmaxf(__builtin_fmaf(g, inv, t), t));
+          const bool need = expired && !(g > 0.0f);
+          if (need) mask |= 1u << k;
+          if (__any(need)) wmask |= 1u << k;
+        }
+      }
+      temin = te[0];
+#pragma unroll
+      for (int j = 1; j < KL; ++j) temin = __builtin_fminf(temin, te[j]);
+    }
     int k;
-    const float d = S.dist(p, k);
+    const float d = S.dist_mask(p, mask, wmask, k);
+    dprev = d;
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
