@@ -14,11 +14,13 @@
 //     distance is strictly smaller; the hit's colour / id / material are read
 //     from the winning entry after the march (the colour at the same point);
 //   * every float operation is the IEEE one the GLSL specifies:
-//     correctly rounded sqrt and division throughout, no contraction — the
-//     specialised kernel's exactness arguments (bounded culling, linear exits,
-//     proven-exact sqrt / reciprocal sequences over bounded domains) depend on
-//     the built-in scene's geometry and are not used here.
-//
+//     correctly rounded sqrt (sqrt_cr_nonneg, proven equal to the IEEE sqrt on
+//     [0, FLT_MAX]) and division, no contraction;
+//   * the shortcuts are the generic forms of the specialised kernel's proofs,
+//     from per-entry bounding balls and plane bounds computed on the host
+//     (rm::exit_bounds): provable miss / shadow exits (table_exit_T), lazy
+//     per-entry culling along marches (tmarch) and per-point culling (dist).
+//     Each only skips work whose result is proven not to change (d, best).
 // For the reference scene (rm_default_scene) the image equals the built-in
 // kernel's bit for bit (tests/test_gpu_scene.py); other tables are checked
 // against the oracle's table mode (oracle/rm_oracle.c rmo_render_scene).
@@ -46,7 +48,7 @@ using rm::TABLE_WORDS;
 #define RM_TABLE_LAZY 1
 #endif
 #ifndef RM_TABLE_FAST_SQRT
-#define RM_TABLE_FAST_SQRT 0
+#define RM_TABLE_FAST_SQRT 1
 #endif
 // Correctly rounded sqrt of a sum of squares (x >= 0, +inf or NaN).  The fast
 // form is sqrt_cr_nonneg (exact on [0, FLT_MAX], rm_fastmath.hpp) with +inf
@@ -223,60 +225,51 @@ __device__ __forceinline__ float table_exit_T(const float* ex, float c, float hm
   return T;
 }
 
-struct THit {
-  float t;  // -1: the dummy RayHit {-1, 0, -1, 1.0} (glsl:128)
-  int id;
-  float material;
-  f3 color;
-};
-
-// RayMarch glsl:125-142 / reflectedRay glsl:144-161
-template <bool COUNT>
-__device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
-  const float tmax = reflected ? 200.0f : 400.0f;
-  const int nmax = reflected ? 256 : 512;
-  float t = 0.0f;
-  // provable miss (table_exit_T): production stops there; the counting build
-  // runs on and poisons the colour with NaN should the ray hit after all
-  const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
-  bool proven = false;
-  // Lazy culling along the ray (RM_TABLE_LAZY; the generic form of scene_lazy,
-  // rm_scene.hpp): slot j tracks entry k_j (rm::exit_bounds) with an expiry
-  // te[j] before which k_j is proven strictly above the minimum.  A re-test at
-  // p = p(t) bounds k_j below by its ball, lb = |p - c'| - R, and the minimum
-  // above by U = min(the planes' values at p, d_prev (1 + L |rd|) + sl): the
-  // previous step moved p by |rd| d_prev and the minimum is L-Lipschitz.  With
-  // sl = 2 sigma (|p|_1 + |ro|_1 + S) covering the float error of both sides
-  // (and of p(t) itself), k_j stays above the minimum while
-  // t' - t < g / ((1 + L) |rd| + 2 sigma |rd|_1), g = lb - U - sl (the second
-  // term: the slack's growth along the ray); g <= 0 evaluates k_j now.  Untracked entries and planes are evaluated at every
-  // step (EX_EVAL_MASK).  Lanes whose te has not expired re-test for free and
-  // keep the later expiry.  The negated compares send NaN rays (degenerate
-  // uniforms) through the re-test, whose NaN bound evaluates every entry.
-  constexpr int KL = rm::EX_MAX_SLOTS;
-  const float* ex = S.exits();
-  const int ns = RM_TABLE_LAZY ? (int)ex[rm::EX_NSLOTS] : 0;
-  const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
-  const uint32_t always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
-  const float INF = __builtin_huge_valf();
+// Lazy culling along a march (RM_TABLE_LAZY; the generic form of scene_lazy,
+// rm_scene.hpp) for p(t) = ro + rd t with t growing by the returned distance
+// after every step (tmarch, tshadow).  Slot j tracks entry k_j (rm::exit_bounds)
+// with an expiry te[j] before which k_j is proven strictly above the minimum.
+// A re-test at p = p(t) bounds k_j below by its ball, lb = |p - c'| - R, and
+// the minimum above by U = min(the planes' values at p, d_prev (1 + L |rd|) +
+// sl): the previous step moved p by |rd| d_prev (d_prev >= 0: a march that goes
+// on past a step has a non-negative distance there) and the minimum is
+// L-Lipschitz.  With sl = 2 sigma (|p|_1 + |ro|_1 + S) covering the float error
+// of both sides (and of p(t) itself), k_j stays above the minimum while
+// t' - t < g / ((1 + L) |rd| + 2 sigma |rd|_1), g = lb - U - sl (the second
+// term: the slack's growth along the ray); g <= 0 evaluates k_j now.
+// Untracked entries and planes are evaluated at every step (EX_EVAL_MASK).
+// Lanes whose te has not expired re-test for free and keep the later expiry.
+// The negated compares send NaN rays (degenerate uniforms) through the
+// re-test, whose NaN bound evaluates every entry.
+struct TLazy {
+  static constexpr int KL = rm::EX_MAX_SLOTS;
+  const float* ex;
+  int ns;
+  uint32_t always;
   float te[KL];
+  float temin, sig2, sl0, inv, grow, dprev;
+
+  __device__ __forceinline__ TLazy(const Table& S, f3 ro, f3 rd) {
+    const float INF = __builtin_huge_valf();
+    ex = S.exits();
+    ns = RM_TABLE_LAZY ? (int)ex[rm::EX_NSLOTS] : 0;
+    const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
+    always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
 #pragma unroll
-  for (int j = 0; j < KL; ++j) te[j] = j < ns ? -INF : INF;
-  float temin = ns > 0 ? -INF : INF;
-  const float lip = ex[rm::EX_LIP], sig2 = 2.0f * ex[rm::EX_SIGMA];
-  const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
-  const float rd1 = ((fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z)) * (1.0f + 0x1p-16f);
-  const float sl0 = (((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z)) + ex[rm::EX_S]) * (1.0f + 0x1p-16f);
-  // the slack grows by sig2 |rd|_1 per unit of t
-  const float inv = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf((1.0f + lip) * rdl + sig2 * rd1) * (1.0f - 0x1p-16f);
-  const float grow = (__builtin_fmaf(lip, rdl, 1.0f) + sig2 * rd1) * (1.0f + 0x1p-10f);
-  float dprev = INF;
-  for (int i = 0; i < nmax; ++i) {
-    if (t > T) {
-      if (!COUNT) break;
-      proven = true;
-    }
-    const f3 p = add(ro, muls(rd, t));
+    for (int j = 0; j < KL; ++j) te[j] = j < ns ? -INF : INF;
+    temin = ns > 0 ? -INF : INF;
+    const float lip = ex[rm::EX_LIP];
+    sig2 = 2.0f * ex[rm::EX_SIGMA];
+    const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+    const float rd1 = ((fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z)) * (1.0f + 0x1p-16f);
+    sl0 = (((fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z)) + ex[rm::EX_S]) * (1.0f + 0x1p-16f);
+    // the slack grows by sig2 |rd|_1 per unit of t
+    inv = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf((1.0f + lip) * rdl + sig2 * rd1) * (1.0f - 0x1p-16f);
+    grow = (__builtin_fmaf(lip, rdl, 1.0f) + sig2 * rd1) * (1.0f + 0x1p-10f);
+    dprev = INF;
+  }
+  // sdf(p(t)) and its opU winner; p = ro + rd t as the caller computed it.
+  __device__ __forceinline__ float dist(const Table& S, f3 p, float t, int& best) {
     uint32_t mask = always, wmask = always;
     if (ns > 0 && __any(!(t < temin))) {
       const float sl = sig2 * (((fabsf(p.x) + fabsf(p.y)) + fabsf(p.z)) + sl0) * (1.0f + 0x1p-10f);
@@ -303,9 +296,37 @@ __device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
 #pragma unroll
       for (int j = 1; j < KL; ++j) temin = __builtin_fminf(temin, te[j]);
     }
+    dprev = S.dist_mask(p, mask, wmask, best);
+    return dprev;
+  }
+};
+
+struct THit {
+  float t;  // -1: the dummy RayHit {-1, 0, -1, 1.0} (glsl:128)
+  int id;
+  float material;
+  f3 color;
+};
+
+// RayMarch glsl:125-142 / reflectedRay glsl:144-161
+template <bool COUNT>
+__device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
+  const float tmax = reflected ? 200.0f : 400.0f;
+  const int nmax = reflected ? 256 : 512;
+  float t = 0.0f;
+  // provable miss (table_exit_T): production stops there; the counting build
+  // runs on and poisons the colour with NaN should the ray hit after all
+  const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
+  bool proven = false;
+  TLazy lz(S, ro, rd);
+  for (int i = 0; i < nmax; ++i) {
+    if (t > T) {
+      if (!COUNT) break;
+      proven = true;
+    }
+    const f3 p = add(ro, muls(rd, t));
     int k;
-    const float d = S.dist_mask(p, mask, wmask, k);
-    dprev = d;
+    const float d = lz.dist(S, p, t, k);
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
@@ -337,13 +358,14 @@ __device__ float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) 
   float res = 1.0f, t = 0.0f;
   const float c_sh = (F.k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / F.k * (1.0f + 0x1p-12f);
   const float T = table_exit_T(S.exits(), c_sh, 0.001f, ro, rd);
+  TLazy lz(S, ro, rd);
   for (int i = 0; i < 16; ++i) {
     if (t > T) {  // the remaining steps are no-ops (table_exit_T)
       if (COUNT) c.shadow += 16 - i;
       return res;
     }
     int k;
-    const float h = S.dist(add(ro, muls(rd, t)), k);
+    const float h = lz.dist(S, add(ro, muls(rd, t)), t, k);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
     res = gmin(res, F.k * h / t);
