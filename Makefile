@@ -22,8 +22,13 @@ LIBRM    := $(PKG)/librm.so
 ORACLE   := oracle/_build/librm_oracle.so
 DRIVER   := $(PKG)/rm_frameloop
 
-RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_table.hip $(CSRC)/rm_host.cpp
-RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp include/rm_api.h
+RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_table.hip $(CSRC)/rm_jit.hip $(CSRC)/rm_host.cpp
+RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp $(CSRC)/rm_jit.hpp include/rm_api.h
+# The table kernel's sources, embedded in librm.so for hiprtc (rm_jit.hip), under
+# the names they #include each other by.
+JIT_SRCS := rm_table.hip=$(CSRC)/rm_table.hip rm_internal.hpp=$(CSRC)/rm_internal.hpp \
+            rm_scene.hpp=$(CSRC)/rm_scene.hpp rm_fastmath.hpp=$(CSRC)/rm_fastmath.hpp \
+            ../../include/rm_api.h=include/rm_api.h
 
 .PHONY: all librm oracle driver goldens clean
 all: librm oracle driver
@@ -35,12 +40,20 @@ $(PKG)/build/%.o: $(CSRC)/%.hip $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(PKG)/build/rm_jit_src.inc: $(CSRC)/rm_table.hip $(RM_HDRS) $(PKG)/tools/embed_sources.py
+	@mkdir -p $(dir $@)
+	python3 $(PKG)/tools/embed_sources.py $@ $(JIT_SRCS)
+
+$(PKG)/build/rm_jit.o: $(CSRC)/rm_jit.hip $(RM_HDRS) $(PKG)/build/rm_jit_src.inc
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -I$(PKG)/build -c $< -o $@
+
 $(PKG)/build/rm_host.o: $(CSRC)/rm_host.cpp $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 
-$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_table.o $(PKG)/build/rm_host.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_table.o $(PKG)/build/rm_jit.o $(PKG)/build/rm_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lhiprtc
 
 $(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h
 	@mkdir -p $(dir $@)

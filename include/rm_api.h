@@ -27,8 +27,10 @@
 #ifndef RM_API_H
 #define RM_API_H
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -226,6 +228,19 @@ int rm_default_scene(rm_primitive *out, int32_t capacity, int32_t *n);
 int rm_set_scene(rm_ctx *ctx, const rm_primitive *prims, int32_t n);
 /* The table in use (*n = 0: the built-in scene). */
 int rm_get_scene(const rm_ctx *ctx, rm_primitive *out, int32_t capacity, int32_t *n);
+/* enable != 0: tables render with kernels compiled for the table itself
+ * (hiprtc, at this call for the current table and at every later
+ * rm_set_scene; the analogue of the reference compiling its shader at run time,
+ * CreateCompute shader.hpp:186-197).  Same image as the generic table kernel;
+ * compiles are cached per process and device.  A failed compile returns
+ * RM_ERR_HIP with the compiler log in rm_last_error and leaves the scene as it
+ * was.  enable == 0: the generic (LDS-staged) table kernel. */
+int rm_scene_specialize(rm_ctx *ctx, int enable);
+/* Diagnostics: the code object rm_scene_specialize would load for this table
+ * on `arch` (e.g. "gfx950"), compiled without a device.  *size = its size;
+ * out == NULL queries the size only. */
+int rm_jit_code_object(const rm_primitive *prims, int32_t n, const char *arch, void *out,
+                       size_t capacity, size_t *size);
 
 /* ---- device-side interop (plain pointers; for stream/collective plumbing) - */
 /* Use an external stream (hipStream_t passed as void*); NULL = own stream. */

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "rm_internal.hpp"
+#include "rm_jit.hpp"
 #include "rm_scene.hpp"
 
 namespace rm {
@@ -57,6 +58,8 @@ struct rm_ctx {
   int nprims = 0;                 // 0: the built-in scene and its specialised kernel
   std::vector<rm_primitive> scene;     // the table as given (rm_get_scene)
   std::vector<uint32_t> scene_words;   // host copy of d_scene (source of the async upload)
+  bool specialize = false;             // rm_scene_specialize: tables render with hiprtc kernels
+  const rm::JitTable* jit = nullptr;   // the current table's specialised kernels, or null
   bool dispatched = false;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -66,6 +69,7 @@ struct rm_ctx {
   bool graph_on = false;
   int graph_aa = -1;  // AA value the graphs were captured for (grid shape depends on it)
   int graph_table = -1;  // whether the graph holds the table kernel (1) or the built-in one (0)
+  const rm::JitTable* graph_jit = nullptr;  // the specialised table kernels captured, if any
   rm_graph_slot gs;
   std::string err;
 };
@@ -415,7 +419,8 @@ int rm_dispatch(rm_ctx* c) {
   }
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   // a runtime scene table renders with the table kernel whatever the variant
-  hipError_t e = c->nprims ? rm::launch_table(F, c->cfg.counters != 0, c->stream)
+  hipError_t e = c->nprims ? (c->jit ? rm::launch_table_jit(c->jit, F, c->cfg.counters != 0, c->stream)
+                                      : rm::launch_table(F, c->cfg.counters != 0, c->stream))
                  : (kernel == RM_KERNEL_PIXEL)
                      ? rm::launch_pixel(F, c->cfg.counters != 0, c->stream)
                      : rm::launch_wavequeue(F, c->cfg.counters != 0, c->stream, c->num_cus);
@@ -533,7 +538,9 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   int rc = RM_OK;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess) {
-    const hipError_t e1 = F.nprims ? rm::launch_table(F, false, cs) : rm::launch_pixel(F, false, cs);
+    const hipError_t e1 = !F.nprims ? rm::launch_pixel(F, false, cs)
+                          : c->jit ? rm::launch_table_jit(c->jit, F, false, cs)
+                                   : rm::launch_table(F, false, cs);
     e = hipStreamEndCapture(cs, &g.graph);
     if (e == hipSuccess) e = e1;
   }
@@ -550,6 +557,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   }
   c->graph_aa = F.aa;
   c->graph_table = F.nprims ? 1 : 0;
+  c->graph_jit = F.nprims ? c->jit : nullptr;
   return RM_OK;
 }
 
@@ -575,7 +583,8 @@ int rm_graph_dispatch(rm_ctx* c) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   rmd::Frame F = make_frame(c);
-  if ((F.aa != c->graph_aa || (F.nprims ? 1 : 0) != c->graph_table) &&
+  if ((F.aa != c->graph_aa || (F.nprims ? 1 : 0) != c->graph_table ||
+       (F.nprims ? c->jit : nullptr) != c->graph_jit) &&
       (rc = graph_capture(c, F)) != RM_OK)
     return rc;
   rm_graph_slot& g = c->gs;
@@ -612,6 +621,7 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
   if (!prims && n == 0) {  // back to the built-in scene
     c->nprims = 0;
     c->scene.clear();
+    c->jit = nullptr;
     return RM_OK;
   }
   std::vector<uint32_t> words(rm::scene_words(n > 0 && n <= RM_MAX_PRIMITIVES ? n : 0));
@@ -619,6 +629,12 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
   if (rm::compile_scene(prims, n, words.data(), &why) != RM_OK) return fail(c, RM_ERR_INVALID, why);
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
+  // compile first: a table whose specialisation fails leaves the context as it was
+  const rm::JitTable* jit = nullptr;
+  if (c->specialize) {
+    std::string err;
+    if ((rc = rm::jit_table(words.data(), n, &jit, err)) != RM_OK) return fail(c, rc, err);
+  }
   if (!c->d_scene) {
     RM_HIP(c, hipMalloc(&c->d_scene, rm::scene_words(RM_MAX_PRIMITIVES) * sizeof(uint32_t)));
   }
@@ -631,6 +647,27 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
                            hipMemcpyHostToDevice, c->stream));
   c->scene.assign(prims, prims + n);
   c->nprims = n;
+  c->jit = jit;
+  return RM_OK;
+}
+
+int rm_scene_specialize(rm_ctx* c, int enable) {
+  if (!c) return RM_ERR_INVALID;
+  c->specialize = enable != 0;
+  if (!c->specialize) {
+    c->jit = nullptr;
+    return RM_OK;
+  }
+  if (!c->nprims || c->jit) return RM_OK;
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  std::string err;
+  const rm::JitTable* jit = nullptr;
+  if ((rc = rm::jit_table(c->scene_words.data(), c->nprims, &jit, err)) != RM_OK) {
+    c->specialize = false;
+    return fail(c, rc, err);
+  }
+  c->jit = jit;
   return RM_OK;
 }
 

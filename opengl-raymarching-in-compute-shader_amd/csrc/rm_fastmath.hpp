@@ -4,7 +4,9 @@
 // tools/exhaustive_fp.hip; the proof log is committed in profiles/.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 namespace rmd {
 

@@ -1,8 +1,17 @@
 // rm_internal.hpp — declarations shared by librm's translation units.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <cstddef>
 #include <cstdint>
+#else  // hiprtc (rm_jit.hip): the fixed-width types live in __hip_internal
+typedef __hip_internal::int8_t int8_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+#endif
 
 #include "../../include/rm_api.h"
 

@@ -1,0 +1,29 @@
+// rm_jit.hpp — hiprtc specialisation of the scene-table kernels (rm_jit.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "rm_internal.hpp"
+
+namespace rmd {
+struct Frame;
+}
+
+namespace rm {
+
+// k_table_{pixel,sample}<counters> compiled for one table: fn[aa][counters].
+struct JitTable {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+};
+
+// Compiles (or finds in the process-wide cache) the table kernels for the
+// compiled table words[0..scene_words(n)) on the current device.  RM_OK, or an
+// RM_ERR_* code with err set (the hiprtc log on a compile error).
+int jit_table(const uint32_t* words, int32_t n, const JitTable** out, std::string& err);
+// The same grid and block as launch_table (rm_table.hip); no dynamic LDS.
+hipError_t launch_table_jit(const JitTable* j, const rmd::Frame& F, bool counters, hipStream_t s);
+
+}  // namespace rm

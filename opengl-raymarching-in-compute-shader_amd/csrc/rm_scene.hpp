@@ -13,8 +13,10 @@
 //     (the x*0 and z*0 terms are signed zeros that cannot change the sum).
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "rm_fastmath.hpp"
 

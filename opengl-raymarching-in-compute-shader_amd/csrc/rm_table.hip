@@ -24,10 +24,26 @@
 // For the reference scene (rm_default_scene) the image equals the built-in
 // kernel's bit for bit (tests/test_gpu_scene.py); other tables are checked
 // against the oracle's table mode (oracle/rm_oracle.c rmo_render_scene).
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 #include "rm_internal.hpp"
 #include "rm_scene.hpp"
+
+// RM_TABLE_STATIC: this file compiled at rm_set_scene time by hiprtc
+// (rm_jit.cpp) for one table, whose compiled words (rm::compile_scene) come as
+// the constant array RM_TS_WORDS[scene_words(RM_TS_N)] of the generated header.
+// Every entry loop is then unrolled over a compile-time table: types, masks and
+// parameters fold into the instruction stream (no LDS staging, no type switch).
+#ifdef RM_TABLE_STATIC
+#include "rm_table_static.h"
+#define RM_TS_UNROLL _Pragma("unroll")
+#define RM_TS_INLINE __forceinline__  // (the unrolled bodies would otherwise become calls)
+#else
+#define RM_TS_UNROLL
+#define RM_TS_INLINE
+#endif
 
 #ifndef RM_TABLE_LDS
 #define RM_TABLE_LDS 1  // 0: read the table through the scalar cache instead of LDS
@@ -96,7 +112,11 @@ __device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float
 
 struct Table {
   const float* t;  // LDS (or global) copy of the compiled table
+#ifdef RM_TABLE_STATIC
+  static constexpr int n = RM_TS_N;
+#else
   int n;
+#endif
   float blend, omblend;
 
   __device__ __forceinline__ const float* exits() const { return t + n * TABLE_WORDS; }
@@ -122,6 +142,7 @@ struct Table {
     const float INF = __builtin_huge_valf();
     float U = INF, slack = 0.0f;
     if (RM_TABLE_CULL) {
+      RM_TS_UNROLL
       for (int k = 0; k < n; ++k)
         if (type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(entry(k), RM_PRIM_PLANE, p, blend, omblend));
       const float* ex = exits();
@@ -130,6 +151,7 @@ struct Table {
     }
     float d = INF;
     best = 0;
+    RM_TS_UNROLL
     for (int k = 0; k < n; ++k) {
       const float* P = entry(k);
       // (spheres: the exact value costs no more than the bound)
@@ -152,8 +174,14 @@ struct Table {
   __device__ __forceinline__ float dist_mask(f3 p, uint32_t mask, uint32_t wave, int& best) const {
     float d = __builtin_huge_valf();
     best = 0;
+#ifdef RM_TABLE_STATIC
+    RM_TS_UNROLL
+    for (int k = 0; k < n; ++k) {
+      if (!((wave >> k) & 1u)) continue;
+#else
     for (; wave; wave &= wave - 1u) {
       const int k = __builtin_ctz(wave);
+#endif
       if (!((mask >> k) & 1u)) continue;
       const float dk = prim_dist(entry(k), type(k), p, blend, omblend);
       const bool keep = d < dk;
@@ -274,8 +302,14 @@ struct TLazy {
     if (ns > 0 && __any(!(t < temin))) {
       const float sl = sig2 * (((fabsf(p.x) + fabsf(p.y)) + fabsf(p.z)) + sl0) * (1.0f + 0x1p-10f);
       float U = __builtin_fmaf(dprev, grow, sl);
+#ifdef RM_TABLE_STATIC
+      RM_TS_UNROLL
+      for (int k = 0; k < S.n; ++k)
+        if (S.type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(S.entry(k), RM_PRIM_PLANE, p, S.blend, S.omblend));
+#else
       for (uint32_t pm = __float_as_uint(ex[rm::EX_PLANE_MASK]); pm; pm &= pm - 1u)
         U = gmin(U, prim_dist(S.entry(__builtin_ctz(pm)), RM_PRIM_PLANE, p, S.blend, S.omblend));
+#endif
 #pragma unroll
       for (int j = 0; j < KL; ++j) {
         if (j < ns && __any(!(t < te[j]))) {
@@ -310,7 +344,7 @@ struct THit {
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161
 template <bool COUNT>
-__device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
+__device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   float t = 0.0f;
@@ -342,7 +376,7 @@ __device__ THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
 
 // GetNormal glsl:278-288
 template <bool COUNT>
-__device__ f3 tnormal(const Table& S, f3 pos, TCnt& c) {
+__device__ RM_TS_INLINE f3 tnormal(const Table& S, f3 pos, TCnt& c) {
   if (COUNT) c.normals++;
   int k;
   const float c0 = S.dist(pos, k);
@@ -354,7 +388,7 @@ __device__ f3 tnormal(const Table& S, f3 pos, TCnt& c) {
 
 // softshadow glsl:201-216
 template <bool COUNT>
-__device__ float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
+__device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   float res = 1.0f, t = 0.0f;
   const float c_sh = (F.k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / F.k * (1.0f + 0x1p-12f);
   const float T = table_exit_T(S.exits(), c_sh, 0.001f, ro, rd);
@@ -377,7 +411,7 @@ __device__ float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) 
 // bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
 // the colour unchanged (glsl:181, 189-190): the loop stops there.
 template <bool COUNT>
-__device__ f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 normal, f3 color,
+__device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 normal, f3 color,
                       const THit& primary, TCnt& c) {
   float prevMat = primary.material;
   f3 prevColor = primary.color;
@@ -408,7 +442,7 @@ __device__ f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 norm
 
 // render glsl:218-251
 template <bool COUNT>
-__device__ f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
+__device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   const THit h = tmarch<COUNT>(S, ro, rd, false, c);
   if (h.t != -1.0f) {
@@ -429,9 +463,14 @@ __device__ f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
 // Stage the table into LDS (one-wave workgroups: the barrier is cheap).
 __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   Table S;
-  S.n = F.nprims;
   S.blend = F.blend;
   S.omblend = F.omblend;
+#ifdef RM_TABLE_STATIC
+  (void)lds;
+  S.t = reinterpret_cast<const float*>(RM_TS_WORDS);
+  return S;
+#else
+  S.n = F.nprims;
   if (RM_TABLE_LDS) {
     for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
     __syncthreads();
@@ -440,6 +479,7 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
     S.t = F.scene;
   }
   return S;
+#endif
 }
 
 __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
@@ -525,6 +565,7 @@ __global__ __launch_bounds__(64) void k_table_sample(Frame F) {
 
 }  // namespace rmd
 
+#ifndef RM_TABLE_STATIC
 namespace rm {
 
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s) {
@@ -546,3 +587,4 @@ hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s) {
 }
 
 }  // namespace rm
+#endif

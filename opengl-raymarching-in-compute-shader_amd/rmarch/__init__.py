@@ -194,6 +194,9 @@ _SIGS = {
     "rm_default_scene": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
     "rm_set_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32]),
     "rm_get_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
+    "rm_scene_specialize": (C.c_int, [_P, C.c_int]),
+    "rm_jit_code_object": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.c_char_p, C.c_void_p,
+                                     C.c_size_t, C.POINTER(C.c_size_t)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(rm_uniforms)]),
 }
@@ -436,6 +439,10 @@ class Renderer:
             return
         tbl = (rm_primitive * len(prims))(*prims)
         _check(lib().rm_set_scene(self.handle, tbl, len(prims)), self.handle)
+
+    def specialize_scene(self, on: bool = True) -> None:
+        """Render tables with kernels compiled for the table (hiprtc; rm_scene_specialize)."""
+        _check(lib().rm_scene_specialize(self.handle, int(on)), self.handle)
 
     def get_scene(self) -> list:
         n = C.c_int32(0)

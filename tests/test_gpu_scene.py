@@ -205,3 +205,74 @@ def test_table_exits_match_oracle(rm, oracle, gpu, seed, nplanes):
     _compare(ref, got, f"seed {seed}")
     prod = _render(rm, u, W, H, scene=scene, counters=False)
     np.testing.assert_array_equal(prod["rgba32f"], got["rgba32f"])
+
+
+# Specialised table kernels (rm_scene_specialize: hiprtc compiles rm_table.hip
+# for the table itself, rm_jit.hip).  Same source and flags, so the images,
+# counters and per-pixel sdf counts must equal the generic table kernel's (and,
+# for the reference scene, the built-in kernel's) bit for bit.
+def _render_spec(rm, u, W, H, scene, counters=True, **kw):
+    with rm.Renderer(W, H, outputs=OUT, counters=counters, **kw) as r:
+        r.specialize_scene(True)
+        r.set_scene(scene)
+        r.dispatch(u)
+        out = {"rgba8": r.read_rgba8(), "rgba32f": r.read_rgba32f()}
+        if counters:
+            out["counters"] = r.counters()
+            out["sdf_counts"] = r.sdf_counts()
+    return out
+
+
+def _same(a, b):
+    np.testing.assert_array_equal(a["rgba32f"], b["rgba32f"])
+    np.testing.assert_array_equal(a["rgba8"], b["rgba8"])
+    if "counters" in a:
+        assert a["counters"] == b["counters"]
+        np.testing.assert_array_equal(a["sdf_counts"], b["sdf_counts"])
+
+
+@pytest.mark.parametrize("case", CASES[:5], ids=lambda c: f"f{c[0]}_b{c[1]}_aa{int(c[2])}_s{c[3]}")
+def test_specialised_default_table_equals_builtin(rm, gpu, case):
+    f, b, aa, sm = case
+    u = rm.sweep_uniforms(f, 120, b, aa, sm)
+    for counters in (True, False):
+        _same(_render_spec(rm, u, 160, 96, rm.default_scene(), counters=counters),
+              _render(rm, u, 160, 96, counters=counters))
+
+
+@pytest.mark.parametrize("seed,nplanes", [(4, None), (5, None), (6, None), (102, 2), (105, 5)])
+def test_specialised_tables_equal_generic(rm, gpu, seed, nplanes):
+    scene = random_scene(rm, seed, nplanes=nplanes)
+    f, b, aa, sm = [(10, 2, True, 0), (60, 3, False, 0), (100, 5, True, 1)][seed % 3]
+    u = rm.sweep_uniforms(f, 120, b, aa, sm)
+    for counters in (True, False):
+        _same(_render_spec(rm, u, 96, 64, scene, counters=counters),
+              _render(rm, u, 96, 64, scene=scene, counters=counters))
+
+
+def test_specialise_toggle_and_graph(rm, gpu):
+    """Toggling specialisation and switching tables re-captures the graph."""
+    a, b = rm.default_scene(), random_scene(rm, 7)
+    frames = [rm.sweep_uniforms(f, 120, 3, True, 0) for f in (0, 60)]
+    want = {}
+    for name, sc in (("a", a), ("b", b)):
+        for i, u in enumerate(frames):
+            want[name, i] = _render(rm, u, 80, 48, scene=sc, counters=False)["rgba32f"]
+    with rm.Renderer(80, 48, outputs=OUT) as r:
+        r.set_scene(a)
+        r.specialize_scene(True)  # compiles for the current table
+        r.graph_enable(True)
+        for i, u in enumerate(frames):
+            r.graph_dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba32f(), want["a", i])
+        r.set_scene(b)  # compiles b; the graph holds a's kernel and must re-capture
+        for i, u in enumerate(frames):
+            r.graph_dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba32f(), want["b", i])
+        r.specialize_scene(False)  # back to the generic kernel
+        r.graph_dispatch(frames[1])
+        np.testing.assert_array_equal(r.read_rgba32f(), want["b", 1])
+        r.set_scene(a)
+        r.specialize_scene(True)  # the cached module: no second compile
+        r.dispatch(frames[0])
+        np.testing.assert_array_equal(r.read_rgba32f(), want["a", 0])

@@ -78,3 +78,31 @@ def test_oracle_rejects_bad_tables(rm, oracle):
     tbl = (rm.rm_primitive * 33)()
     assert L.rmo_render_scene(C.byref(u), tbl, 33, 4, 4, None, 4, None, out.ctypes.data, None,
                               None, None, 1) == -1
+
+
+def _code_object(rm, scene, arch=b"gfx950"):
+    tbl = (rm.rm_primitive * len(scene))(*scene)
+    size = C.c_size_t(0)
+    rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, None, 0, C.byref(size))
+    if rc != 0:
+        return rc, b""
+    buf = C.create_string_buffer(size.value)
+    rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, buf, size.value, C.byref(size))
+    return rc, buf.raw
+
+
+def test_table_specialises_without_a_device(rm):
+    """rm_scene_specialize's hiprtc compile (rm_jit.hip) runs here, without a GPU:
+    the embedded rm_table.hip compiles for gfx950 with the table folded in, and
+    the code object holds the four table kernels."""
+    rc, co = _code_object(rm, rm.default_scene())
+    assert rc == 0 and co[:4] == b"\x7fELF"
+    for name in (b"k_table_pixelILb0E", b"k_table_pixelILb1E", b"k_table_sampleILb0E", b"k_table_sampleILb1E"):
+        assert name in co
+    moved = rm.default_scene()
+    moved[0].center[0] = 14.0
+    rc2, co2 = _code_object(rm, moved)
+    assert rc2 == 0 and co2 != co  # the table is compiled into the code
+    bad = rm.default_scene()
+    bad[0].type = 9
+    assert _code_object(rm, bad)[0] == rm.RM_ERR_INVALID
