@@ -121,10 +121,11 @@ def main() -> int:
     ap.add_argument("--pipeline", type=int, default=1,
                     help="N > 1: gather frame f on a second stream while frame f+1 renders "
                          "(double-buffered shard images); 0 = render, gather, assemble in turn")
-    ap.add_argument("--scene", default="builtin", choices=["builtin", "table"],
+    ap.add_argument("--scene", default="builtin", choices=["builtin", "table", "table-spec"],
                     help="table = the reference scene as a runtime scene table (rm_set_scene with "
-                         "rm_default_scene: the k_table_* kernels, SURVEY 8(f) row 4); the image "
-                         "is the built-in scene's")
+                         "rm_default_scene: the k_table_* kernels, SURVEY 8(f) row 4); table-spec = "
+                         "the same with kernels compiled for the table (rm_scene_specialize, hiprtc, "
+                         "before the timed region); the image is the built-in scene's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=2,
                     help="cpu_baseline renders every k-th row of one frame")
@@ -174,10 +175,17 @@ def main() -> int:
     shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if ws > 1 else {}
     rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
           for _ in range(nfl)]
-    scene = rm.default_scene() if args.scene == "table" else None
+    scene = rm.default_scene() if args.scene in ("table", "table-spec") else None
+    spec = args.scene == "table-spec"
+
+    def use_scene(rj):
+        if spec:
+            rj.specialize_scene(True)
+        rj.set_scene(scene)
+
     if scene is not None:
         for rj in rs:
-            rj.set_scene(scene)
+            use_scene(rj)
     r = rs[0]
     if ws > 1:
         R = args.row_block
@@ -303,7 +311,7 @@ def main() -> int:
                      row_block=args.row_block if ws > 1 else 0, shard=rank if ws > 1 else 0,
                      nshards=ws) as rc:
         if scene is not None:
-            rc.set_scene(scene)
+            use_scene(rc)
         seen = {}
         for k in range(args.steps):
             f = (args.warmup + k) % SWEEP_FRAMES
@@ -317,7 +325,7 @@ def main() -> int:
     kname = ("k_sample" if cfg["aa"] else "k_pixel") if args.kernel == "pixel" else "k_wavequeue"
     if scene is not None:
         kname = "k_table_sample" if cfg["aa"] else "k_table_pixel"
-    pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}")
+    pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}" + ("-spec" if spec else ""))
     traffic = int(pmc["hbm_bytes_per_launch"]) if pmc else None
     # executed VALU issue rate: wave64 VALU instructions x 64 lanes / time, against
     # the lane-instruction peak (157.3 TFLOP/s counts an FMA as 2 -> 78.65 T/s)
@@ -358,7 +366,7 @@ def main() -> int:
         last = args.warmup + args.steps - 1
         with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local) as rf:
             if scene is not None:
-                rf.set_scene(scene)
+                use_scene(rf)
             rf.dispatch(uniforms(last))
             full = rf.read_rgba8()
         d = np.abs(frame.cpu().numpy().astype(np.int16) - full.astype(np.int16))
@@ -381,7 +389,8 @@ def main() -> int:
             "dtype": "f32",
             "data": "synthetic (camera sweep S(120), SURVEY 8(d))",
             "config": {"workload": f"cfg{args.config}: {cfg['desc']}"
-                                   + (" (scene table)" if scene is not None else ""), "width": W, "height": H,
+                                   + (" (scene table)" if scene is not None and not spec else "")
+                                   + (" (scene table, specialised)" if spec else ""), "width": W, "height": H,
                        "bounces": cfg["bounces"], "aa": cfg["aa"],
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
                        "kernel": kname, "hipgraph": bool(use_graph), "frames_in_flight": nfl,

@@ -9,7 +9,9 @@ W, H, b, aa, sm = {3: (3840, 2160, 3, True, 0), 2: (1920, 1080, 1, False, 0),
                    1: (512, 512, 0, False, 1), 4: (3840, 2160, 5, True, 0)}[cfg]
 k = rm.RM_KERNEL_WAVEQUEUE if kname == "wavequeue" else rm.RM_KERNEL_PIXEL
 with rm.Renderer(W, H, kernel=k) as r:
-    if kname == "table":  # the reference scene as a runtime table (k_table_* kernels)
+    if kname == "table-spec":  # the same, with kernels compiled for the table (hiprtc)
+        r.specialize_scene(True)
+    if kname in ("table", "table-spec"):  # the reference scene as a runtime table (k_table_* kernels)
         r.set_scene(rm.default_scene())
     for f in range(nfr):
         r.dispatch(rm.sweep_uniforms(10 + f, 120, b, aa, sm))
