@@ -1,6 +1,6 @@
 """Interleaved A/B of kernel time per frame: librm.so and tools/variants/librm_*.so.
 
-  python tools/ab_kernel.py [--cfg 3] [--rounds 4] [--frames 30] [--table] [variant.so ...]
+  python tools/ab_kernel.py [--cfg 3] [--rounds 4] [--frames 30] [--table] [--spec] [variant.so ...]
 
 Each (round, variant) runs in its own process (RM_LIBRM selects the library);
 the variants alternate within every round, so box drift hits them alike.  Each
@@ -21,13 +21,15 @@ CFGS = {1: (512, 512, 0, False, 1), 2: (1920, 1080, 1, False, 0), 3: (3840, 2160
         4: (3840, 2160, 5, True, 0), 5: (7680, 4320, 3, True, 0)}
 
 
-def child(cfg, frames, table):
+def child(cfg, frames, table, spec=False):
     sys.path.insert(0, os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd"))
     import rmarch as rm
 
     W, H, b, aa, sm = CFGS[cfg]
     with rm.Renderer(W, H) as r:
-        if table:
+        if spec:
+            r.specialize_scene(True)
+        if table or spec:
             r.set_scene(rm.default_scene())
         r.enable_timing(True)
         for f in range(3):
@@ -46,10 +48,11 @@ def main():
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--table", action="store_true", help="the reference scene through the table kernel")
+    ap.add_argument("--spec", action="store_true", help="the same, specialised for the table (hiprtc)")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     if a.child:
-        return child(a.cfg, a.frames, a.table)
+        return child(a.cfg, a.frames, a.table, a.spec)
     libs = a.libs or ([os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd/librm.so")]
                       + sorted(p for p in glob.glob(os.path.join(ROOT, "tools/variants/librm_*.so"))
                                if "librm_stats" not in p))
@@ -58,7 +61,7 @@ def main():
         for p in libs:
             env = dict(os.environ, RM_LIBRM=p)
             out = subprocess.run([sys.executable, __file__, "--child", "--cfg", str(a.cfg), "--frames",
-                                  str(a.frames)] + (["--table"] if a.table else []), env=env, capture_output=True, text=True, timeout=120)
+                                  str(a.frames)] + (["--table"] if a.table else []) + (["--spec"] if a.spec else []), env=env, capture_output=True, text=True, timeout=120)
             if out.returncode != 0:
                 sys.stderr.write(out.stderr)
                 sys.exit(out.returncode)

@@ -18,7 +18,14 @@ for f in rm_api rm_kernels rm_wavequeue rm_table; do
   /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/$f.hip" -o "$b/$f.o" &
 done
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
+if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed the table sources
+  c=$src/$pkg/csrc
+  python3 "$src/$pkg/tools/embed_sources.py" "$b/rm_jit_src.inc" rm_table.hip=$c/rm_table.hip \
+    rm_internal.hpp=$c/rm_internal.hpp rm_scene.hpp=$c/rm_scene.hpp rm_fastmath.hpp=$c/rm_fastmath.hpp \
+    ../../include/rm_api.h=$src/include/rm_api.h
+  /opt/rocm/bin/hipcc $flags -I"$b" -c "$c/rm_jit.hip" -o "$b/rm_jit.o" &
+fi
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o -lhiprtc
 rm -rf "$b"; [ "$src" != "$root" ] && rm -rf "$src"
 echo "$out/librm_$name.so"
