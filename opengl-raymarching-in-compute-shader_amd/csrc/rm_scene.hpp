@@ -386,12 +386,31 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
 //   t_j < t_i + (LB_k - plane(p_i) - slack) / (|rd| + rd.y) * (1 - 2^-10)
 // (|rd| + rd.y >= 0; level and downward rays get 2x and more).  te_k is the
 // later of the two expiries; both are valid, so their max is.
+// Third budget, for a primitive the ray moves away from (RM_DIR_BUDGET).
+// f(t) = |p(t) - c| is convex along the ray, so f(t_j) >= f(t_i) + f'(t_i)(t_j - t_i)
+// with f'(t_i) = rd.(p_i - c) / |p_i - c|.  When rd.(p_i - c) >= 0 (checked with
+// a 2 |rd| slack margin, far above the float error of p_i and of the dot), LB_k
+// does not decrease from t_i on, and the gap closes at |rd| + s1 at most (the
+// minimum's growth and the slack's) instead of 2 |rd| + s1:
+//   te_k = t_i + (LB_k - U_i - slack) / |rd| * (1 - 2^-10);
+// against the plane, at rd.y + s1 instead of |rd| + rd.y, and never when
+// rd.y + s1 <= 0 (a downward ray past a primitive never re-tests it again):
+//   te_k = t_i + (LB_k - plane(p_i) - slack) / (rd.y + s1) * (1 - 2^-10).
+#ifndef RM_DIR_BUDGET
+#define RM_DIR_BUDGET 0  // measured slower (cfg3 +8.5 %, plane term alone +7 %): off
+#endif
+#ifndef RM_DIR_G
+#define RM_DIR_G 1  // 0: only the plane term uses the direction (A/B)
+#endif
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
   float s0, s1;  // slack(t) = s0 + s1 t >= 2^-14 (|ro|_1 + |rd| t + 64)  (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
+#if RM_DIR_BUDGET
+  float invq;    // (1 - 2^-10) / (rd.y + s1) (rounded down), or 2^100 when rd.y + s1 <= 0
+#endif
   float tb;      // t of the last step that entered the re-test block
   int idb;       // the opU id found there
 };
@@ -433,6 +452,11 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
+#if RM_DIR_BUDGET
+  // rd.y + s1 rounds within 2^-24 of the exact sum; v_rcp within 1 ulp
+  const float q = rd.y + s1;
+  c.invq = q > 0.0f ? (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(q) * (1.0f - 0x1p-16f) : 0x1p100f;
+#endif
   c.s0 = s0;
   c.s1 = s1;
   c.tb = -1.0f;
@@ -500,7 +524,7 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       m = vmin(m, v);
     };
     // re-test k; returns true when k must be evaluated exactly at this step
-    auto retest = [&](float x, float R, float& te, int k) -> bool {
+    auto retest = [&](float x, float R, float& te, int k, float nd) -> bool {
       RM_STAT(1);
       RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
@@ -510,7 +534,14 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       // expired lane and the idle one.  t + max(b1, b2, 0) == max(t + b1, t + b2, t)
       // (rounding is monotone); the fmas round once instead of twice, inside the
       // budgets' 2^-10 margin.
-#if RM_TE_FMA
+#if RM_DIR_BUDGET
+      // nd = rd.(p - c_k): nd * inv2v >= slack  =>  nd >= 2 |rd| slack (inv2v <= 1/(2|rd|))
+      const bool away = nd * inv2v >= slack;
+      const float tn = vmax3(__builtin_fmaf((RM_DIR_G && away) ? g + g : g, inv2v, t),
+                             __builtin_fmaf(lb - pl, away ? lc.invq : invp, t), t);
+      const bool expired = t >= te;
+      te = te_max(te, tn);
+#elif RM_TE_FMA
       const float tn = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), t);
       const bool expired = t >= te;
       te = te_max(te, tn);
@@ -525,35 +556,37 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     const Offs o = offsets(p);
     if (RM_LZ_ANY(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
-      if (retest(x0, 3.0f, lc.te[0], 0)) {
+      if (retest(x0, 3.0f, lc.te[0], 0, (rd.x * o.ax + rd.y * o.ay) + rd.z * o.az)) {
         RM_STAT(10);
         take(sqrt_core(x0) - 3.0f, 0, lc.te[0]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
-      if (retest(x1, 3.0f, lc.te[1], 1)) {
+      if (retest(x1, 3.0f, lc.te[1], 1, (rd.x * o.bx + rd.y * o.ay) + rd.z * o.az)) {
         RM_STAT(11);
         take(sqrt_core(x1) - 3.0f, 1, lc.te[1]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
-      if (retest(xs, R_BLEND_LO, lc.te[2], 2)) {
+      if (retest(xs, R_BLEND_LO, lc.te[2], 2, (rd.x * o.cx + rd.y * o.ay) + rd.z * o.az)) {
         RM_STAT(12);
         take(sd_blend(o, xs, blend, omblend), 4, lc.te[2]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3,
+                 (rd.x * o.cx + rd.y * o.ay) + rd.z * tz)) {
         RM_STAT(13);
         take(sd_torus(o, tz), 5, lc.te[3]);
       }
     }
     if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4)) {
+      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4,
+                 (rd.x * kx + rd.y * ky) + rd.z * kz)) {
         RM_STAT(14);
         take(sd_capsule(o, p), 6, lc.te[4]);
       }
