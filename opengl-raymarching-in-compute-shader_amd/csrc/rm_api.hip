@@ -101,6 +101,58 @@ int set_device(rm_ctx* c) {
   return RM_OK;
 }
 
+// Step 0 of every primary ray (rm_scene.hpp PrepSlot), on the host: what k_prep
+// computes, with the same IEEE operations in the same order (x86-64 SSE floats,
+// -ffp-contract=off), so d0 is bit-identical to the device's scene_exact at the
+// camera (sqrt_core / sqrt_cr_nonneg / div_capbb are the IEEE sqrt and divide on
+// the values reached here, rm_fastmath.hpp).  The bounds (slack, LB_k, b1, b2)
+// only need to be valid: their 2^-12 / 2^-18 margins were made for v_sqrt's
+// 1.5 ulp, and the IEEE sqrt is within them.
+void prep_host(const float cam[3], float blend, float omblend, float out[12]) {
+  using namespace rmd;
+  const float px = cam[0], py = cam[1], pz = cam[2];
+  const float ax = px - 15.0f, ay = py, az = pz + 10.0f, bx = px + 25.0f, cx = px + 5.0f;
+  const float ay2 = ay * ay, az2 = az * az, cx2 = cx * cx;
+  const float x0 = (ax * ax + ay2) + az2, x1 = (bx * bx + ay2) + az2, xs = (cx2 + ay2) + az2;
+  const float d0s = std::sqrt(x0) - 3.0f, d1 = std::sqrt(x1) - 3.0f;
+  const float qx = std::fabs(cx) - 3.0f, qy = std::fabs(ay) - 2.5f, qz = std::fabs(az) - 2.5f;
+  const float mx = std::fmax(qx, 0.0f), my = std::fmax(qy, 0.0f), mz = std::fmax(qz, 0.0f);
+  const float box = std::fmin(std::fmax(qx, std::fmax(qy, qz)), 0.0f) +
+                    std::sqrt((mx * mx + my * my) + mz * mz);
+  const float d4 = box * omblend + (std::sqrt(xs) - 3.0f) * blend;
+  const float tz = pz - 10.0f;
+  const float l = std::sqrt(cx2 + ay2) - 2.5f;
+  const float d5 = std::sqrt(l * l + tz * tz) - 0.5f;
+  const float cpx = cx - CAP_AX, cpy = (py + 2.0f) - CAP_AY, cpz = (pz + 30.0f) - CAP_AZ;
+  const float hn = (cpx * CAP_BAX + cpy * CAP_BAY) + cpz * CAP_BAZ;
+  const float h = std::fmin(std::fmax(hn / CAP_BB_HOST, 0.0f), 1.0f);
+  const float ex = cpx - CAP_BAX * h, ey = cpy - CAP_BAY * h, ez = cpz - CAP_BAZ * h;
+  const float d6 = std::sqrt((ex * ex + ey * ey) + ez * ez) - 1.0f;
+  const float d7 = py + 5.5f;
+  const float ds[6] = {d0s, d1, d4, d5, d6, d7};
+  float d = ds[0];
+  bool nan = false;
+  for (float v : ds) {
+    nan = nan || std::isnan(v);
+    d = v < d ? v : d;
+  }
+  const float HI = 1.0f + 0x1p-12f;
+  const float sl = 0x1p-14f * (((std::fabs(px) + std::fabs(py)) + std::fabs(pz)) * HI + 64.0f) * HI;
+  const float sx = px - SH_CX, sy = py - SH_CY, sz = pz - SH_CZ;
+  const float rc = std::fma(std::sqrt((sx * sx + sy * sy) + sz * sz), HI, 0x1p-18f);
+  const float kx = px - CAP_MX, ky = py - CAP_MY, kz = pz - CAP_MZ;
+  const float x[5] = {x0, x1, xs, (cx2 + ay2) + tz * tz, (kx * kx + ky * ky) + kz * kz};
+  const float R[5] = {3.0f, 3.0f, R_BLEND_LO, R_TORUS, R_CAPSULE};
+  std::memset(out, 0, 12 * sizeof(float));
+  out[PREP_VALID] = (!nan && d > 0.0f && d <= 400.0f) ? 1.0f : 0.0f;
+  out[PREP_D0] = d;
+  out[PREP_SLACK] = sl;
+  out[PREP_PL] = (py + 5.5f) + sl;
+  out[PREP_B1] = (rc + SH_RALL + sl + 0.0f) * HI;
+  out[PREP_B2] = ((py + 5.5f) - sl - 0.0f * HI) - 0x1p-19f * (std::fabs(py) + 5.5f + 0.0f + sl);
+  for (int k = 0; k < 5; ++k) out[PREP_LB + k] = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+}
+
 rmd::Frame make_frame(const rm_ctx* c) {
   const rm_uniforms& u = c->u;
   rmd::Frame F;
@@ -138,6 +190,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
   F.queue = c->d_queue;
   F.prep = c->d_prep;
+  prep_host(F.cam_pos, F.blend, F.omblend, F.prepv);
   F.scene = c->nprims ? reinterpret_cast<const float*>(c->d_scene) : nullptr;
   F.nprims = c->nprims;
   rm::pixel_grid(F.width, F.rows, F.aa != 0, &F.grid_x, &F.grid_y);

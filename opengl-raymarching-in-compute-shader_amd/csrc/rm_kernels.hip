@@ -106,10 +106,10 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // per-ray constants; the ro-dependent ones of primary rays come from k_prep
   const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
   float s0, b1, b2;
-  if (RM_PRIMARY_PREP && !reflected && F.prep[PREP_VALID] != 0.0f) {
-    s0 = F.prep[PREP_SLACK];
-    b1 = F.prep[PREP_B1];
-    b2 = F.prep[PREP_B2];
+  if (RM_PRIMARY_PREP && !reflected && prep_at(F, PREP_VALID) != 0.0f) {
+    s0 = prep_at(F, PREP_SLACK);
+    b1 = prep_at(F, PREP_B1);
+    b2 = prep_at(F, PREP_B2);
   } else {
     s0 = ray_s0(ro);
     lin_exit_b(ro, s0, 0.0f, b1, b2);
@@ -122,7 +122,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // (opaque: keeps the compiler from hoisting it, and its registers, out of the loop)
   auto cap_T1 = [&](f3 o, f3 r) {
     float b1c, b2c;
-    if (RM_PRIMARY_PREP && !reflected && F.prep[PREP_VALID] != 0.0f) b1c = F.prep[PREP_B1];
+    if (RM_PRIMARY_PREP && !reflected && prep_at(F, PREP_VALID) != 0.0f) b1c = prep_at(F, PREP_B1);
     else lin_exit_b(o, lc.s0, 0.0f, b1c, b2c);
     return lin_exit_T1(MISS_C, ray_rdl(r), lc.s1, b1c);
   };
@@ -138,11 +138,11 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // once (its distance is exact, its bounds as the block would form them).
   // Each lane only turns the bounds into expiries with its own |rd|: the
   // re-test of scene_lazy with U = d0 (<= the block's running minimum).
-  if (!reflected && F.prep[PREP_VALID] != 0.0f) {
-    const float d0 = F.prep[PREP_D0], sl = F.prep[PREP_SLACK], pl = F.prep[PREP_PL];
+  if (!reflected && prep_at(F, PREP_VALID) != 0.0f) {
+    const float d0 = prep_at(F, PREP_D0), sl = prep_at(F, PREP_SLACK), pl = prep_at(F, PREP_PL);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const float lb = F.prep[PREP_LB + k];
+      const float lb = prep_at(F, PREP_LB + k);
       const float g = lb - d0 - sl;
       const float bud = __builtin_fmaxf(g * lc.inv2v, (lb - pl) * lc.invp);
       lc.te[k] = (g > 0.0f) ? 0.0f + bud : 0.0f;
@@ -676,7 +676,7 @@ void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy) {
 // kernels read the grid from their arguments, not from the hidden dispatch
 // arguments, so the prologue's tile arithmetic waits for one round of loads.
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
-  hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
+  if (!RM_PREP_HOST) hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
   const dim3 grid(F.grid_x, F.grid_y);
   if (F.aa) {
     if (counters)

@@ -95,6 +95,8 @@ struct Frame {
   unsigned long long* counters;  // 6 x u64 (counter builds)
   uint32_t* queue;       // work-queue head (wave-queue kernel), zeroed per dispatch
   const float* prep;     // step 0 of the primary rays (PrepSlot), written by k_prep
+                         // (RM_PREP_HOST=0 builds only)
+  float prepv[12];       // the same values by value, from the host (RM_PREP_HOST, default)
   const float* scene;    // runtime scene table (rm_set_scene), TABLE_WORDS per primitive, or null
   int32_t nprims;        // entries in `scene`
   int32_t grid_x, grid_y;  // k_pixel / k_sample grid (rm::pixel_grid): ordinary kernel
@@ -428,6 +430,16 @@ enum PrepSlot : int {
   PREP_B2 = 10,
   PREP_COUNT = 11
 };
+// RM_PREP_HOST (default): the host forms these per frame (rm_api.hip prep_host,
+// the same IEEE operations; the bounds only need to be valid, and the IEEE sqrt
+// is within the 2^-12 margins made for v_sqrt) and passes them by value, so the
+// render kernel's prologue has no dependent load and no k_prep launch precedes it.
+#ifndef RM_PREP_HOST
+#define RM_PREP_HOST 1
+#endif
+__device__ __forceinline__ float prep_at(const Frame& F, int k) {
+  return RM_PREP_HOST ? F.prepv[k] : F.prep[k];
+}
 
 // Per-ray constants shared by the lazy culler and the linear exits: |rd| from
 // one v_sqrt (within 1.5 ulp) and the slack line s0 + s1 t, rounded up with
