@@ -136,6 +136,10 @@ def main() -> int:
     import torch.distributed as dist
 
     ws, rank, local = dist_env()
+    # RM_BENCH_FORCE_DIST=1 (tests/test_gpu_bench_dist.py): the sharded, RCCL-gathered
+    # step even at world size 1, so one GPU runs the driver's N > 1 code path and its
+    # RCCL calls (init with device_id, gather, barrier, all-reduce) on hardware
+    dist_on = ws > 1 or os.environ.get("RM_BENCH_FORCE_DIST") == "1"
     if ws != args.gpus:
         if ws == 1 and args.gpus > 1:
             print("bench.py: --gpus N > 1 must be launched with torch.distributed.run",
@@ -147,7 +151,7 @@ def main() -> int:
     backend = os.environ.get("RM_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("RM_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
-    if ws > 1:
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -163,8 +167,8 @@ def main() -> int:
     # Explicit streams (torch's default stream has a NULL handle, which librm would
     # replace by its own stream): each in-flight context renders on its own stream;
     # the RCCL gather and the assembly run on `comm`, ordered by events.
-    nfl = args.inflight if args.inflight > 0 else (3 if ws == 1 else 4)
-    nfl = nfl if (ws == 1 or args.pipeline) else 1
+    nfl = args.inflight if args.inflight > 0 else (3 if not dist_on else 4)
+    nfl = nfl if (not dist_on or args.pipeline) else 1
     streams = [torch.cuda.Stream() for _ in range(nfl)]
     torch.cuda.set_stream(streams[0])
 
@@ -178,7 +182,7 @@ def main() -> int:
             ucache[f] = rm.sweep_uniforms(f, SWEEP_FRAMES, cfg["bounces"], cfg["aa"], cfg["shadow"])
         return ucache[f]
 
-    shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if ws > 1 else {}
+    shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if dist_on else {}
     rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
           for _ in range(nfl)]
     scene = rm.default_scene() if args.scene in ("table", "table-spec") else None
@@ -193,7 +197,7 @@ def main() -> int:
         for rj in rs:
             use_scene(rj)
     r = rs[0]
-    if ws > 1:
+    if dist_on:
         R = args.row_block
         rows_cap = r.rows
         nbuf = nfl if args.pipeline else 1
@@ -212,7 +216,7 @@ def main() -> int:
         outs = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nfl)]
     render_done = [torch.cuda.Event() for _ in range(nfl)]
     gather_done = [torch.cuda.Event() for _ in range(nfl)]
-    if ws > 1:
+    if dist_on:
         for ev in gather_done:
             ev.record(comm)
     for j, rj in enumerate(rs):
@@ -227,7 +231,7 @@ def main() -> int:
         else:
             rs[j].dispatch(uniforms(f))
 
-    gather_list = list(gathered.unbind(0)) if ws > 1 and rank == 0 else None
+    gather_list = list(gathered.unbind(0)) if dist_on and rank == 0 else None
 
     def gather(src):
         if backend == "nccl":
@@ -241,7 +245,7 @@ def main() -> int:
 
     def step(f):
         j = f % nfl
-        if ws == 1:
+        if not dist_on:
             render(j, f)
             return
         if not args.pipeline:
@@ -264,7 +268,7 @@ def main() -> int:
 
     def barrier():
         torch.cuda.synchronize()
-        if ws > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -310,7 +314,7 @@ def main() -> int:
         kernel_time_basis = ("HIP events, the timed frames re-rendered one at a time "
                              "(the timed region overlaps frames)")
     elapsed = t1 - t0
-    if ws > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -321,7 +325,7 @@ def main() -> int:
     ops_total = 0
     cnt_total = None
     with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, counters=True, device=local,
-                     row_block=args.row_block if ws > 1 else 0, shard=rank if ws > 1 else 0,
+                     row_block=args.row_block if dist_on else 0, shard=rank if dist_on else 0,
                      nshards=ws) as rc:
         if scene is not None:
             use_scene(rc)
@@ -351,7 +355,7 @@ def main() -> int:
     # ---- CPU baseline + parity sample (rank 0, N = 1 only) ----
     cpu = None
     parity = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dist_on and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # test/baseline infrastructure only
         f = (args.warmup + args.steps - 1) % SWEEP_FRAMES
@@ -374,7 +378,7 @@ def main() -> int:
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
 
     # ---- N > 1: the assembled frame of the last step against a single-GPU render ----
-    if ws > 1 and rank == 0:
+    if dist_on and rank == 0:
         torch.cuda.synchronize()
         last = args.warmup + args.steps - 1
         with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local) as rf:
@@ -409,7 +413,7 @@ def main() -> int:
                        "kernel": kname, "hipgraph": bool(use_graph), "frames_in_flight": nfl,
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        + (" (pipelined)" if args.pipeline else "")
-                                       if ws > 1 else "single GPU")},
+                                       if dist_on else "single GPU")},
             "fps": round(frames / elapsed, 3),
             # host time to issue the K steps (rank 0): well below ms_per_step = GPU-bound
             "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4),
@@ -432,7 +436,7 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     for rj in rs:
         rj.close()
-    if ws > 1:
+    if dist_on:
         dist.destroy_process_group()
     return 0
 

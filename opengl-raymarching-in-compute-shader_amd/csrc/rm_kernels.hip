@@ -361,6 +361,22 @@ __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, C
   return res;
 }
 
+// RM_LDS_STASH: the bounce loop's colour state and hit point are parked in LDS
+// across each reflected march (volatile accesses: the values leave the VGPRs),
+// so the march has the 64-VGPR budget to itself.  One-wave workgroups: 64 lanes
+// x 9 floats = 2.3 KB per workgroup.
+#ifndef RM_LDS_STASH
+#define RM_LDS_STASH 0
+#endif
+#if RM_LDS_STASH
+// (plain LDS accesses with a compiler memory barrier between the stores and the
+// loads: volatile ones would lose the LDS address space and go through flat)
+__device__ __forceinline__ float* stash_slot() {
+  __shared__ float stash[9 * 64];
+  return stash + (threadIdx.x & 63);
+}
+#endif
+
 // bounce glsl:163-199 (dead tail skipped; see rm_oracle.h "live" counters)
 template <bool COUNT>
 __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 primColor,
@@ -377,7 +393,20 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     int id;
     f3 tcol;
     float dl;
+#if RM_LDS_STASH
+    float* sv = stash_slot();
+    const f3 ro_b = add(pos, muls(normal, 0.001f));
+    sv[0] = color.x; sv[64] = color.y; sv[128] = color.z;
+    sv[192] = prevColor.x; sv[256] = prevColor.y; sv[320] = prevColor.z;
+    sv[384] = pos.x; sv[448] = pos.y; sv[512] = pos.z;
+    asm volatile("" ::: "memory");  // the loads below re-read LDS: the values leave the VGPRs
+    float th = march<COUNT>(F, ro_b, rayDir, true, id, tcol, c, dl);
+    color = mk(sv[0], sv[64], sv[128]);
+    prevColor = mk(sv[192], sv[256], sv[320]);
+    pos = mk(sv[384], sv[448], sv[512]);
+#else
     float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c, dl);
+#endif
 #ifdef RM_DBL_BMARCH
     if (!COUNT) {
       int id2; f3 tc2; float dl2;
@@ -542,6 +571,9 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
 #define RM_SAMPLE_BLOCK 64
 #endif
 constexpr int kSampleWaves = RM_SAMPLE_BLOCK / 64;
+#if RM_LDS_STASH
+static_assert(RM_SAMPLE_BLOCK == 64 && RM_PIXEL_BLOCK == 64, "the LDS stash is sized for one-wave workgroups");
+#endif
 constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : 4;
 constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : 4;
 template <bool COUNT>

@@ -53,3 +53,28 @@ def test_bench_ranks_share_one_gpu(n, args):
     p = d["parity"]
     assert p["assembled_equals_single_gpu"] and p["max_abs_delta_rgba8"] == 0, p
     assert p["pixels_checked"] == d["config"]["width"] * d["config"]["height"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ("--config", "2", "--steps", "4", "--warmup", "2"),
+    ("--config", "3", "--steps", "3", "--warmup", "1", "--pipeline", "0"),
+])
+def test_bench_rccl_path_at_world_size_one(args):
+    """bench.py's N > 1 step with its real RCCL calls (backend "nccl": init with
+    device_id, gather on the comm stream, barrier, all-reduce of the time) at
+    world size 1 (RM_BENCH_FORCE_DIST=1): RCCL refuses two ranks on one GPU, so
+    this is the one-GPU run of the driver's multi-GPU code path."""
+    env = dict(os.environ, RM_BENCH_FORCE_DIST="1", RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.pop("RM_BENCH_BACKEND", None)
+    env.pop("RM_BENCH_DEVICE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and "RCCL gather" in d["config"]["parallelism"]
+    p = d["parity"]
+    assert p["assembled_equals_single_gpu"] and p["max_abs_delta_rgba8"] == 0, p
