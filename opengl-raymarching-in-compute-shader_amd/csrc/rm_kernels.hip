@@ -574,16 +574,23 @@ constexpr int kSampleWaves = RM_SAMPLE_BLOCK / 64;
 #if RM_LDS_STASH
 static_assert(RM_SAMPLE_BLOCK == 64 && RM_PIXEL_BLOCK == 64, "the LDS stash is sized for one-wave workgroups");
 #endif
-constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : 4;
-constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : 4;
+// RM_STW: pixel columns of a one-wave tile (4: 4x4 pixels, 8: 8x2, 16: 16x1)
+#ifndef RM_STW
+#define RM_STW 4
+#endif
+static_assert(RM_STW == 4 || kSampleWaves == 1, "RM_STW != 4 needs one-wave workgroups");
+constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : RM_STW;
+constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : (kSampleWaves == 2 ? 4 : 16 / RM_STW);
 template <bool COUNT>
 __device__ __forceinline__ void sample_body(const Frame& F) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
   const int by = tile_row(blockIdx.y, F.grid_y);
   const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kSampleTileW * 4));
-  const int px = bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
-  const int lrow = by * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
+  const int px = kSampleWaves == 1 ? bx * kSampleTileW + q % RM_STW
+                                   : bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
+  const int lrow = kSampleWaves == 1 ? by * kSampleTileH + q / RM_STW
+                                     : by * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
   if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
