@@ -686,19 +686,28 @@ __global__ __launch_bounds__(64) void k_prep(Frame F) {
 }
 
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
+// One grid row per frame row: the source row (shard, local row) is computed once
+// per workgroup in scalar registers; lanes copy 16 B (4 pixels) each when rows
+// are 16-B aligned (width % 4 == 0), one pixel otherwise.
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
                                                  int height, int row_block, int nshards,
                                                  int rows_cap) {
-  const size_t n = (size_t)width * (size_t)height;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n) return;
-  const int y = (int)(idx / (size_t)width);
-  const int x = (int)(idx - (size_t)y * (size_t)width);
-  const int b = y / row_block;
-  const int r = b % nshards;
-  const int lrow = (b / nshards) * row_block + y % row_block;
-  frame[idx] = gathered[((size_t)r * rows_cap + lrow) * (size_t)width + x];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int y = blockIdx.y; y < height; y += gridDim.y) {  // gridDim.y <= 65535
+    const int b = y / row_block;
+    const int r = b % nshards;
+    const int lrow = (b / nshards) * row_block + y % row_block;
+    const uint32_t* src = gathered + ((size_t)r * rows_cap + lrow) * (size_t)width;
+    uint32_t* dst = frame + (size_t)y * (size_t)width;
+    if (VEC) {
+      if (i < width / 4)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else if (i < width) {
+      dst[i] = src[i];
+    }
+  }
 }
 
 }  // namespace rmd
@@ -745,11 +754,17 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s) {
-  const size_t n = (size_t)width * (size_t)height;
-  const unsigned blocks = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(rmd::k_unshard, dim3(blocks), dim3(256), 0, s,
-                     static_cast<const uint32_t*>(gathered), static_cast<uint32_t*>(frame), width,
-                     height, row_block, nshards, rows_cap);
+  const bool vec = width % 4 == 0;
+  const unsigned per_row = (unsigned)(vec ? width / 4 : width);
+  const dim3 grid((per_row + 255) / 256, (unsigned)(height < 65535 ? height : 65535));
+  const uint32_t* g = static_cast<const uint32_t*>(gathered);
+  uint32_t* f = static_cast<uint32_t*>(frame);
+  if (vec)
+    hipLaunchKernelGGL(rmd::k_unshard<true>, grid, dim3(256), 0, s, g, f, width, height, row_block,
+                       nshards, rows_cap);
+  else
+    hipLaunchKernelGGL(rmd::k_unshard<false>, grid, dim3(256), 0, s, g, f, width, height, row_block,
+                       nshards, rows_cap);
   return hipGetLastError();
 }
 

@@ -137,9 +137,10 @@ def test_kernel_timing(rm, gpu):
 
 @pytest.mark.parametrize("kernel", ["pixel", "wavequeue"])
 @pytest.mark.parametrize("N,R", [(2, 8), (3, 4), (8, 8)])
-def test_shards_assemble_to_the_full_frame(rm, gpu, kernel, N, R):
+@pytest.mark.parametrize("W", [80, 83])  # 16-B row copies / per-pixel copies in k_unshard
+def test_shards_assemble_to_the_full_frame(rm, gpu, kernel, N, R, W):
     import torch
-    W, H = 80, 61
+    H = 61
     k = rm.RM_KERNEL_PIXEL if kernel == "pixel" else rm.RM_KERNEL_WAVEQUEUE
     u = rm.sweep_uniforms(70, 120, 3, True, 0)
     full = render(rm, u, W, H, kernel=k)
