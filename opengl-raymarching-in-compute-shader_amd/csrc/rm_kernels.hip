@@ -501,8 +501,11 @@ __device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 constexpr int kPixelWaves = RM_PIXEL_BLOCK / 64;
 constexpr int kTileW = kPixelWaves >= 2 ? 16 : 8;
 constexpr int kTileH = kPixelWaves == 4 ? 16 : 8;
+#ifndef RM_PIXEL_AA
+#define RM_PIXEL_AA 0
+#endif
 #ifndef RM_PIXEL_MIN_WAVES
-#define RM_PIXEL_MIN_WAVES 5
+#define RM_PIXEL_MIN_WAVES 8
 #endif
 #ifndef RM_SAMPLE_MIN_WAVES
 #define RM_SAMPLE_MIN_WAVES 8
@@ -521,7 +524,9 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
   float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
   if (py >= 0) {
     f3 ro, rd;
-    if (F.aa) {
+    // launch_pixel sends AA frames to k_sample: k_pixel's own 4-sample loop is
+    // compiled only with RM_PIXEL_AA=1 (its accumulators cost registers)
+    if (RM_PIXEL_AA && F.aa) {
 #pragma unroll 1
       for (int s = 0; s < 4; ++s) {
         const float x = F.uvx[px * 5 + 1 + s], y = F.uvy[py * 5 + 1 + s];
