@@ -491,9 +491,20 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
   atomicAdd(&F.counters[5], (unsigned long long)c.lights);
 }
 
+// Waves per SIMD the register allocation must allow.  The per-table specialised
+// bodies fit 64 VGPRs without spills: 8 waves (cfg3 table-spec 2.27 -> 2.11 ms per
+// frame).  The generic kernel needs 91 and spills when forced lower.
+#ifndef RM_TABLE_MIN_WAVES
+#ifdef RM_TABLE_STATIC
+#define RM_TABLE_MIN_WAVES 8
+#else
+#define RM_TABLE_MIN_WAVES 1
+#endif
+#endif
+
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
 template <bool COUNT>
-__global__ __launch_bounds__(64) void k_table_pixel(Frame F) {
+__global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
   const int lane = threadIdx.x;
@@ -524,7 +535,7 @@ __global__ __launch_bounds__(64) void k_table_pixel(Frame F) {
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
 template <bool COUNT>
-__global__ __launch_bounds__(64) void k_table_sample(Frame F) {
+__global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
   const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
