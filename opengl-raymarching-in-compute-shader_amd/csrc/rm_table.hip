@@ -492,8 +492,9 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 }
 
 // Waves per SIMD the register allocation must allow.  The per-table specialised
-// bodies fit 64 VGPRs without spills: 8 waves (cfg3 table-spec 2.27 -> 2.11 ms per
-// frame).  The generic kernel needs 91 and spills when forced lower.
+// kernels at 8 waves (64 VGPRs) spill a little (~40 MB of scratch traffic per cfg3
+// launch, PMC) and are still faster: table-spec 2.27 -> 2.10 ms per frame (7 waves:
+// 2.16).  The generic kernel needs 91 VGPRs and spills far more when forced lower.
 #ifndef RM_TABLE_MIN_WAVES
 #ifdef RM_TABLE_STATIC
 #define RM_TABLE_MIN_WAVES 8
