@@ -494,12 +494,13 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 // Waves per SIMD the register allocation must allow.  The per-table specialised
 // kernels at 8 waves (64 VGPRs) spill a little (~40 MB of scratch traffic per cfg3
 // launch, PMC) and are still faster: table-spec 2.27 -> 2.10 ms per frame (7 waves:
-// 2.16).  The generic kernel needs 91 VGPRs and spills far more when forced lower.
+// 2.16).  The generic kernel (91 VGPRs unbounded, 5 waves) is fastest bounded to
+// 6 waves (80 VGPRs, 8 spills): table 3.87 -> 3.47 ms per frame.
 #ifndef RM_TABLE_MIN_WAVES
 #ifdef RM_TABLE_STATIC
 #define RM_TABLE_MIN_WAVES 8
 #else
-#define RM_TABLE_MIN_WAVES 1
+#define RM_TABLE_MIN_WAVES 6
 #endif
 #endif
 
