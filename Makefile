@@ -16,7 +16,7 @@ ARCH     ?= gfx950
 # sqrt/div by default (-fhip-fp32-correctly-rounded-divide-sqrt).
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-result
-OFLAGS   := -std=c11 -O2 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall -Wextra
+OFLAGS   := -std=c11 -O3 -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall -Wextra
 
 LIBRM    := $(PKG)/librm.so
 ORACLE   := oracle/_build/librm_oracle.so

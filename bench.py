@@ -14,19 +14,22 @@ shadows, 4x supersampling, 1 MI355X.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..5]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Step k of K renders sweep frame floor(k * 120 / K): every run samples the whole
+sweep evenly, so `value` is the sweep mean.
+
 Rank 0 prints ONE JSON line.  Extra objects:
-  roofline     : FP32-VALU roofline of the dominant kernel (k_sample / k_pixel);
-                 achieved = algorithmic ops per launch (SURVEY 8(d) weights x the
-                 exact work counters of the frames rendered) / mean kernel time
-                 measured with HIP events on the launch stream.  The algorithmic
-                 count is the reference's brute-force work (every primitive at
-                 every step); the kernel skips most of it by proof (culling,
-                 early exits), so `executed_valu_frac` (committed PMC
-                 SQ_INSTS_VALU x 64 lanes / time vs the lane-instruction peak)
-                 states how busy the VALU actually is.
-  cpu_baseline : the CPU oracle (a C restatement of the reference shader) on
-                 this host's cores, on a bounded row sample of the same frame;
-                 its rows are also compared with the GPU frame (parity).
+  roofline        : FP32-VALU issue roofline of the dominant kernel (k_sample /
+                    k_pixel): achieved = SQ_INSTS_VALU per launch (committed
+                    rocprofv3 PMC pass over the same sweep frames, profiles/) x 64
+                    lanes / the mean kernel time measured here with HIP events on
+                    the launch stream, against 78.65 T lane-instructions/s.
+  algorithmic_rate: the reference's brute-force op count per kernel
+                    second; the kernel skips most of it by proof, so it is not a
+                    utilisation.
+  cpu_baseline    : the CPU oracle (a C restatement of the reference shader) on
+                    this host's cores, -O3 and -O3 -march=native builds, over the
+                    last timed frame; its rows are also compared with the GPU frame
+                    (parity).
 """
 from __future__ import annotations
 
@@ -61,10 +64,18 @@ CONFIGS = {
 }
 SWEEP_FRAMES = 120
 
+
+def bench_frames(steps: int) -> list:
+    """Sweep frames of the K timed steps: step k renders frame floor(k * 120 / K), so
+    every run samples the whole sweep S(120) evenly (K = 120: every frame once) and
+    `value` is the sweep mean, not the cost of one stretch of it."""
+    return [(k * SWEEP_FRAMES // steps) % SWEEP_FRAMES for k in range(steps)]
+
 # Algorithmic FP32 ops per unit of work, SURVEY 8(d) (counted as written in the
 # GLSL; uniform-only subexpressions excluded).  See DESIGN.md §6.
 OPS = dict(march=116, reflect=116, shadow=117, normal=446, light=90, ray=33)
-VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md), FMA = 2 ops
+VALU_LANE_PEAK_T = VALU_PEAK_TFLOPS / 2  # VALU lane-instructions/s
 HBM_PEAK_GBS = 8000.0      # HBM3E spec
 
 
@@ -90,6 +101,83 @@ def pmc_entry(kernel_name: str, workload: str):
             if kernel_name in k and "hbm_bytes_per_launch" in v:
                 return v, os.path.basename(path)
     return None, None
+
+
+def cpu_share() -> dict:
+    """Logical CPUs of this host (nproc) and those this process may run on: the
+    affinity mask, capped by a cgroup CPU quota (cpu.max) when there is one."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(period)))
+    except (OSError, ValueError):
+        pass
+    share = min(aff, quota) if quota else aff
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "share": share, "model": model}
+
+
+def cpu_baseline(args, cfg, u, f):
+    """The reference's path on this host's cores: the CPU oracle (a C restatement of
+    computeShader.glsl, test/baseline infrastructure) in both BASELINE.md builds,
+    -O3 -ffp-contract=off and the same plus -march=native (compiled here, for this
+    CPU), OpenMP schedule(dynamic,1) over rows.  Returns (cpu_baseline, the default
+    build's rows, the rows rendered)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tempfile
+    import oracle as O  # test/baseline infrastructure only
+    W, H = cfg["width"], cfg["height"]
+    stride = args.cpu_row_stride or (1 if W * H * (4 if cfg["aa"] else 1) * max(cfg["bounces"], 1)
+                                     <= 3840 * 2160 * 4 * 3 else 4)
+    rows = list(range(0, H, stride))
+    sh = cpu_share()
+    threads = args.cpu_threads or sh["share"]
+    variants, ref = {}, None
+    for name in ("O3", "O3 -march=native"):
+        try:
+            L = O.lib() if name == "O3" else O.load(O.build_native(tempfile.mkdtemp(prefix="rmo_")))
+        except Exception as e:  # no compiler on this host: report the default build only
+            variants[name] = {"error": str(e)[:200]}
+            continue
+        c0 = time.perf_counter()
+        res = O.render(u, W, H, rows=rows, nthreads=threads, want_f32=False, want_counts=False, L=L)
+        dt = time.perf_counter() - c0
+        if ref is None:
+            ref = res
+        variants[name] = {"Mpixels_per_s": round(len(rows) * W / dt / 1e6, 4), "wall_s": round(dt, 3)}
+    best = max((v["Mpixels_per_s"] for v in variants.values() if "Mpixels_per_s" in v))
+    sample = (f"sweep frame {f} of {cfg['desc']}: "
+              + ("the whole frame" if stride == 1 else f"every {stride}th row ({len(rows)} rows)")
+              + f", {len(rows) * W} px, one process, {threads} OpenMP threads")
+    cpu = {"value": best, "unit": "Mpixels/s", "cores": sh["share"], "threads": threads,
+           "kind": "port", "sample": sample, "variants": variants,
+           "host": {"nproc_logical": sh["nproc"], "affinity": sh["affinity"],
+                    "cgroup_cpu_quota": sh["cgroup_quota"], "cpu_model": sh["model"]},
+           "note": "cores = logical CPUs this process may use (affinity mask, cgroup quota); "
+                   "value = the faster build"}
+    return cpu, ref, rows
+
+
+def pmc_frames(name):
+    if not name:
+        return None
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", name)))["_meta"].get("frames")
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def dist_env():
@@ -127,9 +215,11 @@ def main() -> int:
                          "the same with kernels compiled for the table (rm_scene_specialize, hiprtc, "
                          "before the timed region); the image is the built-in scene's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-row-stride", type=int, default=2,
-                    help="cpu_baseline renders every k-th row of one frame")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-row-stride", type=int, default=0,
+                    help="cpu_baseline renders every k-th row of one frame (0: the whole "
+                         "frame for configs 1-3, every 4th row for the 8K / 5-bounce ones)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = nproc, capped at the CPUs this process may run on")
     args = ap.parse_args()
 
     import torch
@@ -243,8 +333,11 @@ def main() -> int:
         if rank == 0:
             gathered.copy_(torch.stack(hl).to(gathered.device))
 
+    nstep = [0]  # steps issued so far: step n renders on context n % nfl
+
     def step(f):
-        j = f % nfl
+        j = nstep[0] % nfl
+        nstep[0] += 1
         if not dist_on:
             render(j, f)
             return
@@ -272,23 +365,24 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---- warmup (untimed) ----
+    frames_timed = bench_frames(args.steps)
+    # ---- warmup (untimed): the first W frames of the same list ----
     for k in range(args.warmup):
-        step(k)
+        step(frames_timed[k % args.steps])
     barrier()
 
     # ---- timed region: exactly K steps ----
     # (with frames in flight the kernel time comes from a one-at-a-time re-render
     # below, so no per-launch timing events are recorded in the timed region)
-    for f in range(args.warmup, args.warmup + args.steps):
+    for f in frames_timed:
         uniforms(f)
     for rj in rs:
         rj.enable_timing(nfl == 1)
         rj.kernel_time_ms(reset=True)
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    for f in frames_timed:
+        step(f)
     t_issue = time.perf_counter()
     barrier()
     t1 = time.perf_counter()
@@ -306,8 +400,8 @@ def main() -> int:
         barrier()
         r.enable_timing(True)
         r.kernel_time_ms(reset=True)
-        for k in range(args.steps):
-            render(0, args.warmup + k)
+        for f in frames_timed:
+            render(0, f)
         barrier()
         kernel_ms, launches = r.kernel_time_ms(reset=True)
         r.enable_timing(False)
@@ -330,8 +424,7 @@ def main() -> int:
         if scene is not None:
             use_scene(rc)
         seen = {}
-        for k in range(args.steps):
-            f = (args.warmup + k) % SWEEP_FRAMES
+        for f in frames_timed:
             if f not in seen:
                 rc.dispatch(uniforms(f))
                 seen[f] = rc.counters()
@@ -344,10 +437,17 @@ def main() -> int:
         kname = "k_table_sample" if cfg["aa"] else "k_table_pixel"
     pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}" + ("-spec" if spec else ""))
     traffic = int(pmc["hbm_bytes_per_launch"]) if pmc else None
-    # executed VALU issue rate: wave64 VALU instructions x 64 lanes / time, against
-    # the lane-instruction peak (157.3 TFLOP/s counts an FMA as 2 -> 78.65 T/s)
+    # Roofline of the dominant kernel: the FP32 VALU issue rate.  SQ_INSTS_VALU
+    # (wave64 VALU instructions per launch, committed PMC pass over the bench's own
+    # sweep frames, tools/profile_round.sh) x 64 lanes / the kernel time measured
+    # here, against the lane-instruction peak: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz
+    # x 2 (dual issue) = 157.3 T FP32 ops/s counting an FMA as 2 -> 78.65 T
+    # lane-instructions/s.  frac = SQ_INSTS_VALU x 64 / kernel time / 78.65 T.
     valu_insts = pmc.get("SQ_INSTS_VALU") if pmc else None
     valu_issue = (valu_insts * 64 / (mean_kernel_ms * 1e-3) / 1e12) if valu_insts else None
+    # The reference's brute-force work (SURVEY 8(d) op weights x the exact counters of
+    # the frames timed): the kernel skips most of it by proof, so this rate is not
+    # hardware utilisation and can exceed the peak.
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
     bytes_per_launch = r.rows * W * 4
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
@@ -356,23 +456,10 @@ def main() -> int:
     cpu = None
     parity = None
     if rank == 0 and not dist_on and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O  # test/baseline infrastructure only
-        f = (args.warmup + args.steps - 1) % SWEEP_FRAMES
-        u = uniforms(f)
-        rows = list(range(0, H, max(1, args.cpu_row_stride)))
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        c0 = time.perf_counter()
-        ref = O.render(u, W, H, rows=rows, nthreads=threads, want_f32=False, want_counts=False)
-        c1 = time.perf_counter()
-        cpu = {"value": round(len(rows) * W / (c1 - c0) / 1e6, 4), "unit": "Mpixels/s",
-               "cores": threads, "kind": "port",
-               "sample": f"rows py%{args.cpu_row_stride}==0 of sweep frame {f} "
-                         f"({len(rows)}x{W} px, {cfg['desc']}), {c1 - c0:.2f}s wall, "
-                         f"{(c1 - c0) * threads:.0f} core-s"}
+        cpu, ref, rows = cpu_baseline(args, cfg, uniforms(frames_timed[-1]), frames_timed[-1])
         # GPU frame of the same sweep frame: the last step rendered it into its context's buffer.
         torch.cuda.synchronize()
-        g = outs[(args.warmup + args.steps - 1) % nfl].cpu().numpy()[rows]
+        g = outs[(nstep[0] - 1) % nfl].cpu().numpy()[rows]
         d = np.abs(g.astype(np.int16) - ref["rgba8"].astype(np.int16))
         parity = {"max_abs_delta_rgba8": int(d.max()), "pixels_over_2": int((d.max(-1) > 2).sum()),
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
@@ -380,7 +467,7 @@ def main() -> int:
     # ---- N > 1: the assembled frame of the last step against a single-GPU render ----
     if dist_on and rank == 0:
         torch.cuda.synchronize()
-        last = args.warmup + args.steps - 1
+        last = frames_timed[-1]
         with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local) as rf:
             if scene is not None:
                 use_scene(rf)
@@ -417,18 +504,22 @@ def main() -> int:
             "fps": round(frames / elapsed, 3),
             # host time to issue the K steps (rank 0): well below ms_per_step = GPU-bound
             "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4),
-            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3),
-                         "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
+            "roofline": {"bound": "valu",
+                         "achieved": round(valu_issue, 3) if valu_issue else None,
+                         "peak": VALU_LANE_PEAK_T, "unit": "T VALU lane-instructions/s",
+                         "frac": round(valu_issue / VALU_LANE_PEAK_T, 4) if valu_issue else None,
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "valu_insts_per_launch": valu_insts, "pmc_frames": pmc_frames(traffic_src),
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
                          "kernel_time_basis": kernel_time_basis,
-                         "ops_per_launch": int(ops_total / max(launches, 1)),
-                         "executed_valu_Tlane_ops": round(valu_issue, 3) if valu_issue else None,
-                         "executed_valu_frac": (round(valu_issue / (VALU_PEAK_TFLOPS / 2), 4)
-                                                if valu_issue else None),
                          "hbm_write_GBs": round(hbm_gbs, 2),
                          "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
+            "algorithmic_rate": {"ops_per_launch": int(ops_total / max(launches, 1)),
+                                 "TFLOPs": round(achieved_tflops, 3),
+                                 "vs_fp32_peak": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
+                                 "note": "the reference's brute-force op count (SURVEY 8(d)) per "
+                                         "kernel second; the kernel skips most of that work by "
+                                         "proof, so this is not a utilisation"},
             "work": cnt_total,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -38,42 +38,66 @@ def build() -> str:
     return ORACLE_SO
 
 
+# Compiler flags of the committed recipe (Makefile OFLAGS): no FMA contraction and
+# no fast-math, so every float op is one IEEE op in GLSL source order.
+OFLAGS = ["-std=c11", "-O3", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC"]
+
+
+def build_native(outdir: str) -> str:
+    """The BASELINE.md `-march=native` variant (contraction still off), compiled
+    for THIS host's CPU into `outdir` (bench.py builds it on the machine it runs
+    on; a binary built for another CPU could use instructions this one lacks)."""
+    os.makedirs(outdir, exist_ok=True)
+    out = os.path.join(outdir, "librm_oracle_native.so")
+    subprocess.run(["gcc", *OFLAGS, "-march=native", "-shared", "-o", out,
+                    os.path.join(_HERE, "rm_oracle.c"), "-lm"], check=True)
+    return out
+
+
+def _bind(L: C.CDLL) -> C.CDLL:
+    L.rmo_render.restype = C.c_int
+    L.rmo_render.argtypes = [_PU, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                             C.c_void_p, C.c_void_p, C.POINTER(rm_counters),
+                             C.POINTER(rm_counters), C.c_int32]
+    L.rmo_render_scene.restype = C.c_int
+    L.rmo_render_scene.argtypes = [_PU, C.POINTER(rm_primitive), C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.POINTER(rm_counters),
+                                   C.POINTER(rm_counters), C.c_int32]
+    L.rmo_sdf.argtypes = [_PU, _F3, C.POINTER(rmo_hit)]
+    L.rmo_raymarch.argtypes = [_PU, _F3, _F3, C.c_int32, C.POINTER(rmo_hit),
+                               C.POINTER(C.c_uint32)]
+    L.rmo_get_normal.argtypes = [_PU, _F3, _F3]
+    L.rmo_softshadow.restype = C.c_float
+    L.rmo_softshadow.argtypes = [_PU, _F3, _F3, C.c_float, C.POINTER(C.c_uint32)]
+    L.rmo_point_light.argtypes = [_PU, _F3, _F3, _F3, _F3]
+    L.rmo_cast_ray.argtypes = [_PU, C.c_float, C.c_float, _F3, _F3]
+    L.rmo_render_ray.argtypes = [_PU, _F3, _F3, _F3]
+    L.rmo_pixel.argtypes = [_PU, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                            C.c_float * 4]
+    L.rmo_quantize.restype = C.c_uint8
+    L.rmo_quantize.argtypes = [C.c_float]
+    L.rmo_max_threads.restype = C.c_int
+    return L
+
+
+def load(path: str) -> C.CDLL:
+    """Load an oracle build other than the default one (e.g. build_native's)."""
+    return _bind(C.CDLL(path))
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(ORACLE_SO):
             build()
-        L = C.CDLL(ORACLE_SO)
-        L.rmo_render.restype = C.c_int
-        L.rmo_render.argtypes = [_PU, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
-                                 C.c_void_p, C.c_void_p, C.POINTER(rm_counters),
-                                 C.POINTER(rm_counters), C.c_int32]
-        L.rmo_render_scene.restype = C.c_int
-        L.rmo_render_scene.argtypes = [_PU, C.POINTER(rm_primitive), C.c_int32, C.c_int32,
-                                       C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.POINTER(rm_counters),
-                                       C.POINTER(rm_counters), C.c_int32]
-        L.rmo_sdf.argtypes = [_PU, _F3, C.POINTER(rmo_hit)]
-        L.rmo_raymarch.argtypes = [_PU, _F3, _F3, C.c_int32, C.POINTER(rmo_hit),
-                                   C.POINTER(C.c_uint32)]
-        L.rmo_get_normal.argtypes = [_PU, _F3, _F3]
-        L.rmo_softshadow.restype = C.c_float
-        L.rmo_softshadow.argtypes = [_PU, _F3, _F3, C.c_float, C.POINTER(C.c_uint32)]
-        L.rmo_point_light.argtypes = [_PU, _F3, _F3, _F3, _F3]
-        L.rmo_cast_ray.argtypes = [_PU, C.c_float, C.c_float, _F3, _F3]
-        L.rmo_render_ray.argtypes = [_PU, _F3, _F3, _F3]
-        L.rmo_pixel.argtypes = [_PU, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                                C.c_float * 4]
-        L.rmo_quantize.restype = C.c_uint8
-        L.rmo_quantize.argtypes = [C.c_float]
-        L.rmo_max_threads.restype = C.c_int
-        _lib = L
+        _lib = _bind(C.CDLL(ORACLE_SO))
     return _lib
 
 
 def render(u: rm_uniforms, W: int, H: int, rows: Optional[Sequence[int]] = None,
            nthreads: int = 0, want_f32: bool = True, want_counts: bool = True,
-           scene: Optional[Sequence[rm_primitive]] = None) -> dict:
+           scene: Optional[Sequence[rm_primitive]] = None, L: Optional[C.CDLL] = None) -> dict:
     """Render rows (default: all) with the oracle.  Row 0 = bottom (py = 0).
 
     ``scene``: a runtime scene table (rm_primitive entries) in place of the GLSL's
@@ -87,11 +111,12 @@ def render(u: rm_uniforms, W: int, H: int, rows: Optional[Sequence[int]] = None,
     tail = (W, H, None if rows_arr is None else rows_arr.ctypes.data, n,
             None if f32 is None else f32.ctypes.data, rgba8.ctypes.data,
             None if counts is None else counts.ctypes.data, C.byref(cnt), C.byref(full), nthreads)
+    L = L or lib()
     if scene is None:
-        rc = lib().rmo_render(C.byref(u), *tail)
+        rc = L.rmo_render(C.byref(u), *tail)
     else:
         tbl = (rm_primitive * len(scene))(*scene)
-        rc = lib().rmo_render_scene(C.byref(u), tbl, len(scene), *tail)
+        rc = L.rmo_render_scene(C.byref(u), tbl, len(scene), *tail)
     if rc != 0:
         raise ValueError("rmo_render: bad arguments")
     return {"rgba8": rgba8, "rgba32f": f32, "sdf_counts": counts, "counters": cnt.as_dict(),

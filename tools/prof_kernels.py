@@ -1,19 +1,29 @@
-"""Render a few cfg frames with one kernel variant (driver for rocprofv3 --pmc)."""
+"""Render the bench's sweep frames with one kernel variant (driver for rocprofv3 --pmc).
+
+  python tools/prof_kernels.py KIND CFG STEPS
+KIND: pixel | wavequeue | table | table-spec.  The frames are bench.py's own
+(bench_frames(STEPS): step k renders sweep frame floor(k * 120 / STEPS)), one
+launch each, so the per-launch PMC means describe the benched workload.
+"""
+import os
 import sys
-sys.path.insert(0, 'opengl-raymarching-in-compute-shader_amd')
-import rmarch as rm
-kname = sys.argv[1] if len(sys.argv) > 1 else "wavequeue"
-cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-nfr = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-W, H, b, aa, sm = {3: (3840, 2160, 3, True, 0), 2: (1920, 1080, 1, False, 0),
-                   1: (512, 512, 0, False, 1), 4: (3840, 2160, 5, True, 0)}[cfg]
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'opengl-raymarching-in-compute-shader_amd'))
+import rmarch as rm  # noqa: E402
+from bench import CONFIGS, bench_frames  # noqa: E402
+
+kname = sys.argv[1] if len(sys.argv) > 1 else "pixel"
+cfg = CONFIGS[int(sys.argv[2]) if len(sys.argv) > 2 else 3]
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 k = rm.RM_KERNEL_WAVEQUEUE if kname == "wavequeue" else rm.RM_KERNEL_PIXEL
-with rm.Renderer(W, H, kernel=k) as r:
+with rm.Renderer(cfg["width"], cfg["height"], kernel=k) as r:
     if kname == "table-spec":  # the same, with kernels compiled for the table (hiprtc)
         r.specialize_scene(True)
     if kname in ("table", "table-spec"):  # the reference scene as a runtime table (k_table_* kernels)
         r.set_scene(rm.default_scene())
-    for f in range(nfr):
-        r.dispatch(rm.sweep_uniforms(10 + f, 120, b, aa, sm))
+    for f in bench_frames(steps):
+        r.dispatch(rm.sweep_uniforms(f, 120, cfg["bounces"], cfg["aa"], cfg["shadow"]))
     r.synchronize()
-print("done", kname, cfg)
+print("done", kname, sys.argv[2:])

@@ -47,9 +47,13 @@ def main(src, tag, workload="cfg3", dst="profiles"):
             cs["hbm_write_bytes"] = w
             cs["hbm_bytes_per_launch"] = 2 * f + w
     # bench.py matches a summary to its workload through _meta
+    kind, cfg, steps = (os.environ.get("PROF_KIND", "pixel"), os.environ.get("PROF_CFG", "3"),
+                        os.environ.get("PROF_STEPS", "20"))
+    head = os.popen("git rev-parse --short=12 HEAD 2>/dev/null").read().strip()
     out["_meta"] = {"workload": workload, "source": os.path.basename(os.path.normpath(src)),
-                    "passes": "separate rocprofv3 --pmc runs of tools/prof_kernels.py "
-                              + os.environ.get("PROF_KIND", "pixel") + " 3 3"}
+                    "frames": f"bench_frames({steps}) of cfg{cfg}: step k -> sweep frame k*120//{steps}",
+                    "commit": head,
+                    "passes": f"separate rocprofv3 --pmc runs of tools/prof_kernels.py {kind} {cfg} {steps}"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     log = open(os.path.join(src, "bench_traced.log")).read().splitlines()
     line = [l for l in log if l.startswith("{")]
