@@ -180,6 +180,16 @@ def pmc_frames(name):
         return None
 
 
+def comm_ids(n: int, rank: int) -> list:
+    """n RCCL unique ids for rm_comm_init, made on rank 0 (rm_comm_unique_id) and
+    broadcast over the torch.distributed host channel (gloo)."""
+    import torch.distributed as dist
+    ids = [rm.comm_unique_id() for _ in range(n)] if rank == 0 else [None] * n
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast_object_list(ids, src=0)
+    return ids
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -228,24 +238,18 @@ def main() -> int:
     ws, rank, local = dist_env()
     # RM_BENCH_FORCE_DIST=1 (tests/test_gpu_bench_dist.py): the sharded, RCCL-gathered
     # step even at world size 1, so one GPU runs the driver's N > 1 code path and its
-    # RCCL calls (init with device_id, gather, barrier, all-reduce) on hardware
+    # RCCL calls (communicator, gather, assembly inside librm) on hardware
     dist_on = ws > 1 or os.environ.get("RM_BENCH_FORCE_DIST") == "1"
     if ws != args.gpus:
         if ws == 1 and args.gpus > 1:
             print("bench.py: --gpus N > 1 must be launched with torch.distributed.run",
                   file=sys.stderr)
             return 2
-    # Rehearsal knobs (tests/test_gpu_bench_dist.py, one GPU): RM_BENCH_DEVICE puts every
-    # rank on one device, RM_BENCH_BACKEND=gloo gathers through host memory.  The
-    # driver's multi-GPU runs use neither: one rank per GPU, RCCL ("nccl").
-    backend = os.environ.get("RM_BENCH_BACKEND", "nccl")
-    local = int(os.environ.get("RM_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     if dist_on:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        # host-side control only (RCCL ids, barriers, the max over ranks of the time):
+        # the frame data moves inside librm, over its own RCCL communicators
+        dist.init_process_group("gloo")
 
     cfg = CONFIGS[args.config]
     W, H = cfg["width"], cfg["height"]
@@ -254,13 +258,11 @@ def main() -> int:
     if use_graph and kernel == rm.RM_KERNEL_WAVEQUEUE:
         print("bench.py: --graph renders with the default kernel", file=sys.stderr)
         return 2
-    # Explicit streams (torch's default stream has a NULL handle, which librm would
-    # replace by its own stream): each in-flight context renders on its own stream;
-    # the RCCL gather and the assembly run on `comm`, ordered by events.
+    # Frames in flight: consecutive frames go to separate contexts, each with its own
+    # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
+    # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
     nfl = args.inflight if args.inflight > 0 else (3 if not dist_on else 4)
     nfl = nfl if (not dist_on or args.pipeline) else 1
-    streams = [torch.cuda.Stream() for _ in range(nfl)]
-    torch.cuda.set_stream(streams[0])
 
     ucache = {}
 
@@ -275,6 +277,11 @@ def main() -> int:
     shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if dist_on else {}
     rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
           for _ in range(nfl)]
+    if dist_on:
+        # one communicator per in-flight context (rm_comm_init): rank 0 makes the
+        # ids, the host channel carries them; every rank joins in the same order
+        for rj, cid in zip(rs, comm_ids(nfl, rank)):
+            rj.comm_init(cid, ws, rank)
     scene = rm.default_scene() if args.scene in ("table", "table-spec") else None
     spec = args.scene == "table-spec"
 
@@ -287,80 +294,27 @@ def main() -> int:
         for rj in rs:
             use_scene(rj)
     r = rs[0]
-    if dist_on:
-        R = args.row_block
-        rows_cap = r.rows
-        nbuf = nfl if args.pipeline else 1
-        outs = [torch.empty((rows_cap, W, 4), dtype=torch.uint8, device="cuda")
-                for _ in range(nbuf)]
-        gathered = (torch.empty((ws, rows_cap, W, 4), dtype=torch.uint8, device="cuda")
-                    if rank == 0 else None)
-        frame = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
-        comm = torch.cuda.Stream()
-        ru = None
-        if rank == 0:  # assembles on the comm stream (same shard geometry as r)
-            ru = rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local,
-                             row_block=R, shard=0, nshards=ws)
-            ru.set_stream(comm.cuda_stream if args.pipeline else streams[0].cuda_stream)
-    else:
-        outs = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nfl)]
-    render_done = [torch.cuda.Event() for _ in range(nfl)]
-    gather_done = [torch.cuda.Event() for _ in range(nfl)]
-    if dist_on:
-        for ev in gather_done:
-            ev.record(comm)
-    for j, rj in enumerate(rs):
-        rj.set_stream(streams[j].cuda_stream)
-        rj.set_output_rgba8(outs[j % len(outs)].data_ptr())
+    for rj in rs:
         if use_graph:
             rj.graph_enable(True)
 
     def render(j, f):
+        # one frame on context j: render; for N > 1 also the gather on rank 0 and
+        # rank 0's assembly, all inside librm on the context's stream
         if use_graph:
             rs[j].graph_dispatch(uniforms(f))
         else:
             rs[j].dispatch(uniforms(f))
-
-    gather_list = list(gathered.unbind(0)) if dist_on and rank == 0 else None
-
-    def gather(src):
-        if backend == "nccl":
-            dist.gather(src, gather_list=gather_list, dst=0)
-            return
-        host = src.cpu()  # gloo rehearsal: host staging (synchronous on the current stream)
-        hl = [torch.empty_like(host) for _ in range(ws)] if rank == 0 else None
-        dist.gather(host, gather_list=hl, dst=0)
-        if rank == 0:
-            gathered.copy_(torch.stack(hl).to(gathered.device))
 
     nstep = [0]  # steps issued so far: step n renders on context n % nfl
 
     def step(f):
         j = nstep[0] % nfl
         nstep[0] += 1
-        if not dist_on:
-            render(j, f)
-            return
-        if not args.pipeline:
-            render(0, f)
-            gather(outs[0])
-            if rank == 0:
-                ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
-            return
-        # frame f renders on streams[j] into outs[j] once that buffer's previous
-        # gather is done; the gather and the assembly follow on `comm`
-        streams[j].wait_event(gather_done[j])
         render(j, f)
-        render_done[j].record(streams[j])
-        with torch.cuda.stream(comm):
-            comm.wait_event(render_done[j])
-            gather(outs[j])
-            if rank == 0:
-                ru.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
-            gather_done[j].record(comm)
 
     def barrier():
-        torch.cuda.synchronize()
+        torch.cuda.synchronize()  # the device: every librm stream
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
@@ -409,7 +363,7 @@ def main() -> int:
                              "(the timed region overlaps frames)")
     elapsed = t1 - t0
     if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     frames = args.steps
@@ -449,7 +403,7 @@ def main() -> int:
     # the frames timed): the kernel skips most of it by proof, so this rate is not
     # hardware utilisation and can exceed the peak.
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
-    bytes_per_launch = r.rows * W * 4
+    bytes_per_launch = (rm.shard_rows_cap(H, args.row_block, ws) if dist_on else H) * W * 4
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
 
     # ---- CPU baseline + parity sample (rank 0, N = 1 only) ----
@@ -459,7 +413,7 @@ def main() -> int:
         cpu, ref, rows = cpu_baseline(args, cfg, uniforms(frames_timed[-1]), frames_timed[-1])
         # GPU frame of the same sweep frame: the last step rendered it into its context's buffer.
         torch.cuda.synchronize()
-        g = outs[(nstep[0] - 1) % nfl].cpu().numpy()[rows]
+        g = rs[(nstep[0] - 1) % nfl].read_rgba8()[rows]
         d = np.abs(g.astype(np.int16) - ref["rgba8"].astype(np.int16))
         parity = {"max_abs_delta_rgba8": int(d.max()), "pixels_over_2": int((d.max(-1) > 2).sum()),
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
@@ -473,7 +427,8 @@ def main() -> int:
                 use_scene(rf)
             rf.dispatch(uniforms(last))
             full = rf.read_rgba8()
-        d = np.abs(frame.cpu().numpy().astype(np.int16) - full.astype(np.int16))
+        frame = rs[(nstep[0] - 1) % nfl].read_rgba8()  # rank 0: the assembled frame
+        d = np.abs(frame.astype(np.int16) - full.astype(np.int16))
         parity = {"assembled_equals_single_gpu": bool(d.max() == 0),
                   "max_abs_delta_rgba8": int(d.max()), "pixels_checked": int(W * H),
                   "reference": f"single-GPU render of sweep frame {last % SWEEP_FRAMES}"}

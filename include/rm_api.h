@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RM_API_VERSION 1
+#define RM_API_VERSION 2
 
 /* ---- status codes --------------------------------------------------------- */
 #define RM_OK 0
@@ -118,6 +118,18 @@ typedef struct rm_config {
   int32_t row_block;
   int32_t shard;
   int32_t nshards;
+  /* Multi-GPU frames in one process.  ngpus >= 1 makes the
+   * context drive ngpus devices: devices[0..ngpus), or device, device+1, ...
+   * when devices is NULL (device -1 = the current device).  Device i renders
+   * shard i of the interleaved row blocks (row_block rows per block, 0 = 8);
+   * ncclGather over a single-process communicator (ncclCommInitAll) collects
+   * the shards on devices[0], which assembles the frame (k_unshard).  The
+   * setters, rm_dispatch, rm_synchronize, rm_read_rgba8, rm_set_scene and the
+   * graph calls work as on a one-GPU context; the frame lives on devices[0].
+   * RGBA8 output only, no counters, shard/nshards must be 0.  ngpus = 0: one
+   * device, no RCCL (API version 1 behaviour). */
+  int32_t ngpus;
+  const int32_t *devices;
 } rm_config;
 
 typedef struct rm_ctx rm_ctx;
@@ -261,6 +273,27 @@ int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
  * launch count since the last reset (synchronizes). */
 int rm_enable_timing(rm_ctx *ctx, int enable);
 int rm_kernel_time_ms(rm_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+
+/* ---- one rank per process: RCCL-gathered frames -------------
+ * The multi-process form of rm_config.ngpus, for hosts that run one process
+ * per GPU (torch.distributed.run, MPI).  Rank 0 creates an id and broadcasts it
+ * over the host's own channel; every rank then joins its sharded context
+ * (cfg.nshards = nranks, cfg.shard = rank) to the communicator
+ * (ncclCommInitRank: collective, every rank must call it).  From then on
+ * rm_dispatch renders this rank's shard, gathers all shards on rank 0
+ * (ncclGather into rank 0's [nranks][rows_cap][width] buffer; rank 0 renders
+ * its own shard in place) and, on rank 0, assembles the frame (k_unshard), all
+ * on the context's stream.  Rank 0's rm_read_rgba8 / rm_get_output_rgba8 /
+ * rm_set_output_rgba8 then refer to the full height x width frame, the other
+ * ranks' to their packed shard.  rm_dispatch and rm_graph_dispatch are
+ * collective: every rank issues the same sequence.  rm_graph_dispatch captures
+ * render + gather + assembly into one hipGraph per rank (cfg 5).  RGBA8 only. */
+#define RM_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
+int rm_comm_unique_id(void *id, size_t size);
+int rm_comm_init(rm_ctx *ctx, const void *id, int32_t nranks, int32_t rank);
+/* The context's communicator: rank / size (0 / 1 without one), and the devices
+ * a multi-GPU context drives (*ngpus = 1 for a one-GPU context). */
+int rm_comm_info(const rm_ctx *ctx, int32_t *rank, int32_t *nranks, int32_t *ngpus);
 
 /* ---- row sharding helpers (pure functions) ------------------------------- */
 int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);

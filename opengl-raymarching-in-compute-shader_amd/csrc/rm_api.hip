@@ -14,6 +14,7 @@
 #include <utility>
 #include <vector>
 
+#include "rm_comm.hpp"
 #include "rm_internal.hpp"
 #include "rm_jit.hpp"
 #include "rm_scene.hpp"
@@ -29,13 +30,15 @@ hipError_t launch_unshard(const void* gathered, void* frame, int width, int heig
                           int nshards, int rows_cap, hipStream_t s);
 }  // namespace rm
 
-// The graph path: one captured render-kernel node whose by-value frame
-// constants are replaced per frame (hipGraphExecKernelNodeSetParams).
+// The graph path: the captured frame (the render kernel, and for a rank of an
+// RCCL-gathered frame the gather and the assembly after it) whose render node
+// gets the frame's by-value constants per replay (hipGraphExecKernelNodeSetParams).
 struct rm_graph_slot {
   hipGraph_t graph = nullptr;
-  hipGraphNode_t node[4] = {};  // the kernel nodes (k_prep, render), all taking a Frame
-  size_t nodes = 0;
+  hipGraphNode_t render = nullptr;  // the render kernel's node (its argument is a Frame)
   hipGraphExec_t exec = nullptr;
+  const void* send = nullptr;       // buffers the captured gather / assembly use
+  const void* frame = nullptr;
 };
 
 struct rm_ctx {
@@ -71,6 +74,16 @@ struct rm_ctx {
   int graph_table = -1;  // whether the graph holds the table kernel (1) or the built-in one (0)
   const rm::JitTable* graph_jit = nullptr;  // the specialised table kernels captured, if any
   rm_graph_slot gs;
+  // RCCL-gathered frames (rm_comm_init, or one device of a multi-GPU context)
+  ncclComm_t comm = nullptr;
+  bool own_comm = false;      // destroyed with the context
+  bool group_member = false;  // a device of a multi-GPU context: its parent issues the gather
+  bool comm_warm = false;     // a gather has run eagerly (before any graph capture)
+  int crank = 0, cranks = 1;
+  uint8_t* d_gathered = nullptr;  // rank 0: [cranks][rows][width] RGBA8; its own shard renders into slot 0
+  uint8_t* d_frame = nullptr;     // rank 0: the assembled [height][width] frame
+  // a multi-GPU context (rm_config.ngpus): one shard context per device, subs[0] = rank 0
+  std::vector<rm_ctx*> subs;
   std::string err;
 };
 
@@ -99,6 +112,31 @@ int hip_fail(rm_ctx* c, hipError_t e, const char* what) {
 int set_device(rm_ctx* c) {
   RM_HIP(c, hipSetDevice(c->device));
   return RM_OK;
+}
+
+// ---- where images live --------------------------------------------------------------
+// A plain context renders into its RGBA8 image (the caller's, or its own).  Rank 0
+// of an RCCL-gathered frame renders its shard into slot 0 of the gather buffer and
+// its readable image is the assembled frame; the other ranks' is their shard.
+bool comm_root(const rm_ctx* c) { return c->comm && c->crank == 0; }
+uint8_t* render_dst(const rm_ctx* c) {
+  if (!(c->cfg.outputs & RM_OUT_RGBA8)) return nullptr;
+  if (comm_root(c)) return c->d_gathered;
+  return c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8;
+}
+uint8_t* image_rgba8(const rm_ctx* c) {
+  if (!c->subs.empty()) return image_rgba8(c->subs[0]);
+  if (comm_root(c)) return c->ext_rgba8 ? c->ext_rgba8 : c->d_frame;
+  return render_dst(c);
+}
+int image_rows(const rm_ctx* c) {
+  if (!c->subs.empty() || comm_root(c)) return c->cfg.height;
+  return c->rows;
+}
+bool full_frame(const rm_ctx* c) { return c->cfg.nshards <= 1 || !c->subs.empty() || comm_root(c); }
+
+int nccl_fail(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
+  return fail(c, RM_ERR_HIP, std::string(what) + ": " + (r ? r->GetErrorString(e) : "RCCL"));
 }
 
 // Step 0 of every primary ray (rm_scene.hpp PrepSlot), on the host: what k_prep
@@ -184,7 +222,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.shard = c->cfg.shard;
   F.nshards = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
   F.rows = c->rows;
-  F.rgba8 = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
+  F.rgba8 = render_dst(c);
   F.rgba32f = (c->cfg.outputs & RM_OUT_RGBA32F) ? c->d_rgba32f : nullptr;
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
@@ -209,6 +247,17 @@ void graph_release(rm_ctx* c) {
 
 void free_all(rm_ctx* c) {
   graph_release(c);
+  for (rm_ctx* s : c->subs) rm_destroy(s);
+  c->subs.clear();
+  if (c->own_comm && c->comm) {
+    std::string err;
+    if (const rm::Rccl* r = rm::rccl(&err)) (void)r->CommDestroy(c->comm);
+  }
+  c->comm = nullptr;
+  if (c->d_gathered) (void)hipFree(c->d_gathered);
+  if (c->d_frame) (void)hipFree(c->d_frame);
+  c->d_gathered = nullptr;
+  c->d_frame = nullptr;
   if (c->d_rgba8) (void)hipFree(c->d_rgba8);
   if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
   if (c->d_counts) (void)hipFree(c->d_counts);
@@ -239,6 +288,131 @@ int check_uniforms(rm_ctx* c, const rm_uniforms& u) {
     return fail(c, RM_ERR_INVALID, "bounceVar must be in 0..5 (main.cpp:199-204)");
   if (u.shadow_mode != RM_SHADOW_SOFT && u.shadow_mode != RM_SHADOW_HARD)
     return fail(c, RM_ERR_INVALID, "shadow_mode must be RM_SHADOW_SOFT or RM_SHADOW_HARD");
+  return RM_OK;
+}
+
+// Joins a sharded context to a communicator as `rank` of `n`: rank 0 gets the
+// gather buffer (its shard renders into slot 0, so ncclGather runs in place) and
+// the assembled frame.
+int comm_attach(rm_ctx* c, ncclComm_t comm, int rank, int n, bool own, bool member) {
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  c->comm = comm;
+  c->own_comm = own;
+  c->group_member = member;
+  c->crank = rank;
+  c->cranks = n;
+  if (rank == 0) {
+    const size_t shard = (size_t)c->rows * c->cfg.width * 4, frame = (size_t)c->cfg.height * c->cfg.width * 4;
+    RM_HIP(c, hipMalloc(&c->d_gathered, shard * n));
+    RM_HIP(c, hipMalloc(&c->d_frame, frame));
+    RM_HIP(c, hipMemsetAsync(c->d_gathered, 0, shard * n, c->stream));
+    RM_HIP(c, hipMemsetAsync(c->d_frame, 0, frame, c->stream));
+    RM_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->d_rgba8) (void)hipFree(c->d_rgba8);  // rank 0 renders into the gather buffer
+    c->d_rgba8 = nullptr;
+  }
+  graph_release(c);
+  return RM_OK;
+}
+
+int check_comm_config(const rm_config& cfg, const char* who) {
+  if ((cfg.outputs & ~RM_OUT_RGBA8) != 0 || cfg.counters)
+    return fail(nullptr, RM_ERR_INVALID, std::string(who) + ": RCCL-gathered frames are RGBA8 only, "
+                                         "without counters");
+  return RM_OK;
+}
+
+// rm_config.ngpus >= 1: one shard context per device plus a single-process
+// communicator over the devices (ncclCommInitAll).
+int create_multi(rm_ctx** out, const rm_config* cfg) {
+  const int n = cfg->ngpus;
+  int rc = check_comm_config(*cfg, "rm_create");
+  if (rc != RM_OK) return rc;
+  if (cfg->nshards > 1 || cfg->shard != 0)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: ngpus shards by itself (shard/nshards must be 0)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, RM_ERR_NO_DEVICE, "rm_create: no HIP device (librm has no CPU fallback)");
+  std::vector<int> devs(n);
+  int d0 = cfg->device;
+  if (d0 < 0 && hipGetDevice(&d0) != hipSuccess) d0 = 0;
+  for (int i = 0; i < n; ++i) {
+    devs[i] = cfg->devices ? cfg->devices[i] : d0 + i;
+    if (devs[i] < 0 || devs[i] >= ndev)
+      return fail(nullptr, RM_ERR_INVALID, "rm_create: device " + std::to_string(devs[i]) +
+                                               " out of range (" + std::to_string(ndev) + " devices)");
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i])
+        return fail(nullptr, RM_ERR_INVALID, "rm_create: devices must be distinct (one shard per GPU)");
+  }
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(nullptr, RM_ERR_HIP, "rm_create: " + err);
+  rm_ctx* c = new (std::nothrow) rm_ctx();
+  if (!c) return fail(nullptr, RM_ERR_NOMEM, "rm_create: out of host memory");
+  c->cfg = *cfg;
+  c->cfg.outputs = RM_OUT_RGBA8;
+  c->cfg.row_block = cfg->row_block > 0 ? cfg->row_block : 8;
+  c->cfg.nshards = n;
+  c->cfg.shard = 0;
+  c->cfg.devices = nullptr;  // not kept: the caller owns the array
+  c->device = devs[0];
+  c->rows = c->cfg.height;
+  rm_default_uniforms(&c->u);
+  auto bail = [&](int code) {
+    g_create_error = c->err;
+    free_all(c);
+    delete c;
+    return code;
+  };
+  for (int i = 0; i < n; ++i) {
+    rm_config sc = c->cfg;
+    sc.ngpus = 0;
+    sc.device = devs[i];
+    sc.shard = i;
+    rm_ctx* sub = nullptr;
+    if ((rc = rm_create(&sub, &sc)) != RM_OK) {
+      c->err = "rm_create (device " + std::to_string(devs[i]) + "): " + g_create_error;
+      return bail(rc);
+    }
+    c->subs.push_back(sub);
+  }
+  std::vector<ncclComm_t> comms(n, nullptr);
+  ncclResult_t e = r->CommInitAll(comms.data(), n, devs.data());
+  if (e != ncclSuccess) return bail(nccl_fail(c, r, e, "ncclCommInitAll"));
+  for (int i = 0; i < n; ++i) {
+    if ((rc = comm_attach(c->subs[i], comms[i], i, n, true, true)) != RM_OK) {
+      c->err = c->subs[i]->err;
+      for (int j = i + 1; j < n; ++j) (void)r->CommDestroy(comms[j]);
+      return bail(rc);
+    }
+  }
+  c->stream = c->subs[0]->stream;  // the frame's stream (not owned)
+  *out = c;
+  return RM_OK;
+}
+
+// The gather of one rank (ncclGather to rank 0, in place on rank 0).
+int comm_gather(rm_ctx* c) {
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_HIP, err);
+  const size_t count = (size_t)c->rows * c->cfg.width * 4;
+  const void* send = render_dst(c);
+  void* recv = comm_root(c) ? c->d_gathered : nullptr;
+  const ncclResult_t e = r->Gather(send, recv, count, ncclUint8, 0, c->comm, c->stream);
+  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGather");
+  c->comm_warm = true;
+  return RM_OK;
+}
+
+// Rank 0: the gathered shards -> the frame (k_unshard), on the same stream.
+int comm_assemble(rm_ctx* c) {
+  if (!comm_root(c)) return RM_OK;
+  const hipError_t e = rm::launch_unshard(c->d_gathered, image_rgba8(c), c->cfg.width, c->cfg.height,
+                                          c->cfg.row_block, c->cranks, c->rows, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }
 
@@ -278,6 +452,13 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   *out = nullptr;
   if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65536 || cfg->height > 65536)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: width/height must be in 1..65536");
+  if (cfg->ngpus < 0 || cfg->ngpus > 64)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: ngpus must be in 0..64");
+  if (cfg->ngpus >= 1) {
+    if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_WAVEQUEUE)
+      return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
+    return create_multi(out, cfg);
+  }
   if (cfg->outputs & ~(RM_OUT_RGBA8 | RM_OUT_RGBA32F))
     return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown output bits");
   if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_WAVEQUEUE)
@@ -292,6 +473,7 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   rm_ctx* c = new (std::nothrow) rm_ctx();
   if (!c) return fail(nullptr, RM_ERR_NOMEM, "rm_create: out of host memory");
   c->cfg = *cfg;
+  c->cfg.devices = nullptr;  // not kept: the caller owns the array
   if (c->cfg.outputs == 0) c->cfg.outputs = RM_OUT_RGBA8;
   if (c->cfg.nshards <= 1) {
     c->cfg.nshards = 1;
@@ -446,26 +628,34 @@ int rm_get_uniforms(const rm_ctx* c, rm_uniforms* u) {
 }
 
 // ---- dispatch ---------------------------------------------------------------------
-int rm_dispatch(rm_ctx* c) {
-  if (!c) return RM_ERR_INVALID;
+namespace {
+
+// Timing events for the next launch (rm_enable_timing), or nulls.
+int timing_events(rm_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!c->timing) return RM_OK;
+  if (c->ev_used == c->ev_pool.size()) {
+    std::pair<hipEvent_t, hipEvent_t> p;
+    RM_HIP(c, hipEventCreate(&p.first));
+    RM_HIP(c, hipEventCreate(&p.second));
+    c->ev_pool.push_back(p);
+  }
+  *e0 = c->ev_pool[c->ev_used].first;
+  *e1 = c->ev_pool[c->ev_used].second;
+  c->ev_used++;
+  return RM_OK;
+}
+
+// The render kernel of one frame on the context's stream (== glDispatchCompute).
+int render_launch(rm_ctx* c) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   if (c->cfg.counters) {
     RM_HIP(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
   }
   rmd::Frame F = make_frame(c);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->timing) {
-    if (c->ev_used == c->ev_pool.size()) {
-      std::pair<hipEvent_t, hipEvent_t> p;
-      RM_HIP(c, hipEventCreate(&p.first));
-      RM_HIP(c, hipEventCreate(&p.second));
-      c->ev_pool.push_back(p);
-    }
-    e0 = c->ev_pool[c->ev_used].first;
-    e1 = c->ev_pool[c->ev_used].second;
-    c->ev_used++;
-  }
+  hipEvent_t e0, e1;
+  if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
   const int kernel = c->cfg.kernel == RM_KERNEL_AUTO ? RM_KERNEL_PIXEL : c->cfg.kernel;
   if (kernel == RM_KERNEL_WAVEQUEUE) {
     RM_HIP(c, hipMemsetAsync(c->d_queue, 0, 256, c->stream));
@@ -483,8 +673,57 @@ int rm_dispatch(rm_ctx* c) {
   return RM_OK;
 }
 
+int graph_frame(rm_ctx* c);
+
+// A multi-GPU context's frame: every device renders its shard (plainly or from
+// its render-only graph), one grouped ncclGather collects the shards on device
+// 0 (a single-process communicator needs the group), device 0 assembles.
+int multi_frame(rm_ctx* c, bool graph) {
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_HIP, err);
+  for (rm_ctx* s : c->subs) {
+    s->u = c->u;
+    const int rc = graph ? graph_frame(s) : render_launch(s);
+    if (rc != RM_OK) return fail(c, rc, s->err);
+  }
+  ncclResult_t e = r->GroupStart();
+  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGroupStart");
+  int rc = RM_OK;
+  for (rm_ctx* s : c->subs) {
+    if ((rc = set_device(s)) != RM_OK || (rc = comm_gather(s)) != RM_OK) break;
+  }
+  e = r->GroupEnd();
+  if (rc != RM_OK) return fail(c, rc, c->subs.empty() ? "" : c->subs[0]->err);
+  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGroupEnd");
+  if ((rc = set_device(c->subs[0])) != RM_OK || (rc = comm_assemble(c->subs[0])) != RM_OK)
+    return fail(c, rc, c->subs[0]->err);
+  c->dispatched = true;
+  return RM_OK;
+}
+
+}  // namespace
+
+int rm_dispatch(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty()) return multi_frame(c, false);
+  int rc = render_launch(c);
+  if (rc != RM_OK) return rc;
+  // one rank of an RCCL-gathered frame: gather on rank 0, which assembles
+  if (c->comm && !c->group_member) {
+    if ((rc = comm_gather(c)) != RM_OK) return rc;
+    if ((rc = comm_assemble(c)) != RM_OK) return rc;
+  }
+  return RM_OK;
+}
+
 int rm_synchronize(rm_ctx* c) {
   if (!c) return RM_ERR_INVALID;
+  for (rm_ctx* s : c->subs) {
+    const int rc = rm_synchronize(s);
+    if (rc != RM_OK) return fail(c, rc, s->err);
+  }
+  if (!c->subs.empty()) return RM_OK;
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   RM_HIP(c, hipStreamSynchronize(c->stream));
@@ -496,15 +735,20 @@ static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t 
   if (!c || !dst) return RM_ERR_INVALID;
   if (!dev) return fail(c, RM_ERR_STATE, "output format not enabled in rm_config.outputs");
   if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
-  if (flip_y && c->cfg.nshards > 1)
+  if (flip_y && !full_frame(c))
     return fail(c, RM_ERR_INVALID, "flip_y is not defined for a packed shard image");
+  if (!c->subs.empty()) {  // the frame is on device 0, behind every device's stream
+    const int rc = rm_synchronize(c);
+    if (rc != RM_OK) return rc;
+    c = c->subs[0];
+  }
   const size_t w = (size_t)c->cfg.width * bpp;
   if (row_pitch == 0) row_pitch = w;
   if (row_pitch < w) return fail(c, RM_ERR_INVALID, "row_pitch smaller than a row");
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   RM_HIP(c, hipStreamSynchronize(c->stream));
-  const size_t rows = (size_t)c->rows;
+  const size_t rows = (size_t)image_rows(c);
   RM_HIP(c, hipMemcpy2D(dst, row_pitch, dev, w, w, rows, hipMemcpyDeviceToHost));
   if (flip_y) {
     // Row 0 of the device image is the bottom row (quad.hpp:9); flip in place
@@ -524,8 +768,7 @@ static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t 
 
 int rm_read_rgba8(rm_ctx* c, uint8_t* dst, size_t row_pitch, int flip_y) {
   if (!c) return RM_ERR_INVALID;
-  const void* dev = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
-  return read_image(c, dev, 4, dst, row_pitch, flip_y);
+  return read_image(c, image_rgba8(c), 4, dst, row_pitch, flip_y);
 }
 
 int rm_read_rgba32f(rm_ctx* c, float* dst, size_t row_pitch, int flip_y) {
@@ -577,37 +820,52 @@ int rm_read_sdf_counts(rm_ctx* c, uint32_t* dst) {
 }
 
 // ---- hipGraph frame replay -----------------------------------------------------------
-// Captures (once per AA setting: the grid and kernel depend on it) the render
-// kernel launch into a graph.  Each rm_graph_dispatch writes the frame's
-// constants into the kernel node's by-value argument and replays it; the
-// kernel is the same code as rm_dispatch's (k_sample / k_pixel), so the graph
-// path renders identical images at identical register budgets.  Counters and
-// the wave-queue kernel are not available on this path.
+// Captures the frame once per AA setting / scene kernel / buffer set: the render
+// kernel launch, and for one rank of an RCCL-gathered frame (rm_comm_init) the
+// ncclGather and rank 0's assembly after it.  Each replay writes the frame's
+// constants into the render node's by-value argument and launches the graph, so
+// the graph path runs the same kernels as rm_dispatch at the same register
+// budgets.  Counters and the wave-queue kernel are not available on this path.
 static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   graph_release(c);
   rm_graph_slot& g = c->gs;
+  const bool comm = c->comm && !c->group_member;
   hipStream_t cs = nullptr;
   RM_HIP(c, hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  hipStream_t keep = c->stream;
   int rc = RM_OK;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess) {
-    const hipError_t e1 = !F.nprims ? rm::launch_pixel(F, false, cs)
-                          : c->jit ? rm::launch_table_jit(c->jit, F, false, cs)
-                                   : rm::launch_table(F, false, cs);
-    e = hipStreamEndCapture(cs, &g.graph);
-    if (e == hipSuccess) e = e1;
+    e = !F.nprims ? rm::launch_pixel(F, false, cs)
+        : c->jit  ? rm::launch_table_jit(c->jit, F, false, cs)
+                  : rm::launch_table(F, false, cs);
+    // the render node: the one node the next captured operation would depend on
+    hipStreamCaptureStatus st;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    if (e == hipSuccess) e = hipStreamGetCaptureInfo_v2(cs, &st, nullptr, nullptr, &deps, &ndeps);
+    if (e == hipSuccess && ndeps == 1) g.render = deps[0];
+    else if (e == hipSuccess) e = hipErrorInvalidValue;
+    if (e == hipSuccess && comm) {
+      c->stream = cs;  // the gather and the assembly, captured after the render
+      rc = comm_gather(c);
+      if (rc == RM_OK) rc = comm_assemble(c);
+      c->stream = keep;
+    }
+    hipGraph_t gr = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(cs, &gr);
+    g.graph = gr;
+    if (e == hipSuccess) e = e2;
   }
-  size_t n = 4;
-  if (e == hipSuccess) e = hipGraphGetNodes(g.graph, g.node, &n);
-  if (e == hipSuccess && (n < 1 || n > 4)) e = hipErrorInvalidValue;
-  g.nodes = n;
-  if (e == hipSuccess) e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+  if (e == hipSuccess && rc == RM_OK) e = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
   (void)hipStreamDestroy(cs);
-  if (e != hipSuccess) {
-    rc = hip_fail(c, e, "graph capture");
+  if (e != hipSuccess || rc != RM_OK) {
+    if (rc == RM_OK) rc = hip_fail(c, e, "graph capture");
     graph_release(c);
     return rc;
   }
+  g.send = render_dst(c);
+  g.frame = image_rgba8(c);
   c->graph_aa = F.aa;
   c->graph_table = F.nprims ? 1 : 0;
   c->graph_jit = F.nprims ? c->jit : nullptr;
@@ -616,6 +874,14 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
 
 int rm_graph_enable(rm_ctx* c, int enable) {
   if (!c) return RM_ERR_INVALID;
+  for (rm_ctx* s : c->subs) {
+    const int rc = rm_graph_enable(s, enable);
+    if (rc != RM_OK) return fail(c, rc, s->err);
+  }
+  if (!c->subs.empty()) {
+    c->graph_on = enable != 0;
+    return RM_OK;
+  }
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   if (!enable) {
@@ -630,47 +896,59 @@ int rm_graph_enable(rm_ctx* c, int enable) {
   return RM_OK;
 }
 
-int rm_graph_dispatch(rm_ctx* c) {
-  if (!c) return RM_ERR_INVALID;
-  if (!c->graph_on) return fail(c, RM_ERR_STATE, "rm_graph_enable(ctx, 1) first");
+namespace {
+int graph_frame(rm_ctx* c) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   rmd::Frame F = make_frame(c);
+  const bool comm = c->comm && !c->group_member;
+  if (comm && !c->comm_warm) {
+    // RCCL sets a communicator's buffers up on its first operation, which must
+    // not happen inside a capture: the first frame of a rank runs eagerly (every
+    // rank takes the same branch, so the collective sequence matches)
+    return rm_dispatch(c);
+  }
   if ((F.aa != c->graph_aa || (F.nprims ? 1 : 0) != c->graph_table ||
-       (F.nprims ? c->jit : nullptr) != c->graph_jit) &&
+       (F.nprims ? c->jit : nullptr) != c->graph_jit || c->gs.send != render_dst(c) ||
+       c->gs.frame != image_rgba8(c)) &&
       (rc = graph_capture(c, F)) != RM_OK)
     return rc;
   rm_graph_slot& g = c->gs;
   void* args[] = {&F};
-  for (size_t k = 0; k < g.nodes; ++k) {
-    hipKernelNodeParams kp;
-    RM_HIP(c, hipGraphKernelNodeGetParams(g.node[k], &kp));
-    kp.kernelParams = args;
-    kp.extra = nullptr;
-    RM_HIP(c, hipGraphExecKernelNodeSetParams(g.exec, g.node[k], &kp));
-  }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->timing) {
-    if (c->ev_used == c->ev_pool.size()) {
-      std::pair<hipEvent_t, hipEvent_t> p;
-      RM_HIP(c, hipEventCreate(&p.first));
-      RM_HIP(c, hipEventCreate(&p.second));
-      c->ev_pool.push_back(p);
-    }
-    e0 = c->ev_pool[c->ev_used].first;
-    e1 = c->ev_pool[c->ev_used].second;
-    c->ev_used++;
-  }
+  hipKernelNodeParams kp;
+  RM_HIP(c, hipGraphKernelNodeGetParams(g.render, &kp));
+  kp.kernelParams = args;
+  kp.extra = nullptr;
+  RM_HIP(c, hipGraphExecKernelNodeSetParams(g.exec, g.render, &kp));
+  hipEvent_t e0, e1;
+  if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   RM_HIP(c, hipGraphLaunch(g.exec, c->stream));
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
   c->dispatched = true;
   return RM_OK;
 }
+}  // namespace
+
+int rm_graph_dispatch(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  if (!c->graph_on) return fail(c, RM_ERR_STATE, "rm_graph_enable(ctx, 1) first");
+  if (!c->subs.empty()) return multi_frame(c, true);
+  return graph_frame(c);
+}
 
 // ---- runtime scene table ----------------------------------------------------------
 int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
   if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty()) {  // every device renders the same table
+    for (rm_ctx* s : c->subs) {
+      const int rc = rm_set_scene(s, prims, n);
+      if (rc != RM_OK) return fail(c, rc, s->err);
+    }
+    c->nprims = c->subs[0]->nprims;
+    c->scene = c->subs[0]->scene;
+    return RM_OK;
+  }
   if (!prims && n == 0) {  // back to the built-in scene
     c->nprims = 0;
     c->scene.clear();
@@ -706,7 +984,12 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
 
 int rm_scene_specialize(rm_ctx* c, int enable) {
   if (!c) return RM_ERR_INVALID;
+  for (rm_ctx* s : c->subs) {
+    const int rc = rm_scene_specialize(s, enable);
+    if (rc != RM_OK) return fail(c, rc, s->err);
+  }
   c->specialize = enable != 0;
+  if (!c->subs.empty()) return RM_OK;
   if (!c->specialize) {
     c->jit = nullptr;
     return RM_OK;
@@ -737,6 +1020,8 @@ int rm_get_scene(const rm_ctx* c, rm_primitive* out, int32_t capacity, int32_t* 
 // ---- device interop ----------------------------------------------------------------
 int rm_set_stream(rm_ctx* c, void* hip_stream) {
   if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty())
+    return fail(c, RM_ERR_STATE, "a multi-GPU context runs one stream per device (its own)");
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   if (c->own_stream && c->stream) {
@@ -756,6 +1041,10 @@ int rm_set_stream(rm_ctx* c, void* hip_stream) {
 
 int rm_set_output_rgba8(rm_ctx* c, void* device_ptr) {
   if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty()) {  // the frame's destination on device 0
+    const int rc = rm_set_output_rgba8(c->subs[0], device_ptr);
+    return rc == RM_OK ? rc : fail(c, rc, c->subs[0]->err);
+  }
   if (!(c->cfg.outputs & RM_OUT_RGBA8))
     return fail(c, RM_ERR_STATE, "RGBA8 output not enabled in rm_config.outputs");
   c->ext_rgba8 = static_cast<uint8_t*>(device_ptr);
@@ -764,12 +1053,13 @@ int rm_set_output_rgba8(rm_ctx* c, void* device_ptr) {
 
 int rm_get_output_rgba8(rm_ctx* c, void** device_ptr) {
   if (!c || !device_ptr) return RM_ERR_INVALID;
-  *device_ptr = (c->cfg.outputs & RM_OUT_RGBA8) ? (c->ext_rgba8 ? c->ext_rgba8 : c->d_rgba8) : nullptr;
+  *device_ptr = image_rgba8(c);
   return RM_OK;
 }
 
 int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
   if (!c || !gathered_dev || !frame_dev) return RM_ERR_INVALID;
+  if (!c->subs.empty()) return fail(c, RM_ERR_STATE, "a multi-GPU context assembles its own frames");
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   hipError_t e = rm::launch_unshard(gathered_dev, frame_dev, c->cfg.width, c->cfg.height,
@@ -778,14 +1068,20 @@ int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
   return RM_OK;
 }
 
+// A multi-GPU context times device 0's render kernel.
 int rm_enable_timing(rm_ctx* c, int enable) {
   if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty()) return rm_enable_timing(c->subs[0], enable);
   c->timing = enable != 0;
   return RM_OK;
 }
 
 int rm_kernel_time_ms(rm_ctx* c, double* total_ms, int64_t* launches, int reset) {
   if (!c) return RM_ERR_INVALID;
+  if (!c->subs.empty()) {
+    const int rc = rm_kernel_time_ms(c->subs[0], total_ms, launches, reset);
+    return rc == RM_OK ? rc : fail(c, rc, c->subs[0]->err);
+  }
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   for (size_t i = 0; i < c->ev_used; ++i) {
@@ -802,6 +1098,57 @@ int rm_kernel_time_ms(rm_ctx* c, double* total_ms, int64_t* launches, int reset)
     c->total_ms = 0.0;
     c->launches = 0;
   }
+  return RM_OK;
+}
+
+// ---- one rank per process -------------------------------------------------------------
+int rm_comm_unique_id(void* id, size_t size) {
+  if (!id || size < sizeof(ncclUniqueId)) return fail(nullptr, RM_ERR_INVALID, "rm_comm_unique_id: buffer < 128 bytes");
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(nullptr, RM_ERR_HIP, "rm_comm_unique_id: " + err);
+  ncclUniqueId u;
+  const ncclResult_t e = r->GetUniqueId(&u);
+  if (e != ncclSuccess) return fail(nullptr, RM_ERR_HIP, std::string("ncclGetUniqueId: ") + r->GetErrorString(e));
+  std::memcpy(id, &u, sizeof u);
+  return RM_OK;
+}
+
+int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
+  if (!c || !id) return RM_ERR_INVALID;
+  if (!c->subs.empty()) return fail(c, RM_ERR_STATE, "a multi-GPU context has its own communicator");
+  if (c->comm) return fail(c, RM_ERR_STATE, "the context already has a communicator");
+  if (nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(c, RM_ERR_INVALID, "rm_comm_init: rank must be in 0..nranks-1");
+  const int ns = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
+  if (ns != nranks || c->cfg.shard != rank)
+    return fail(c, RM_ERR_INVALID, "rm_comm_init: the context must render shard `rank` of `nranks` "
+                                   "(rm_config.shard / nshards)");
+  if (check_comm_config(c->cfg, "rm_comm_init") != RM_OK) return fail(c, RM_ERR_INVALID, g_create_error);
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_HIP, "rm_comm_init: " + err);
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  ncclComm_t comm = nullptr;
+  const ncclResult_t e = r->CommInitRank(&comm, nranks, u, rank);
+  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclCommInitRank");
+  RM_HIP(c, hipStreamSynchronize(c->stream));  // frames already queued keep their buffers
+  if ((rc = comm_attach(c, comm, rank, nranks, true, false)) != RM_OK) {
+    (void)r->CommDestroy(comm);
+    c->comm = nullptr;
+    return rc;
+  }
+  return RM_OK;
+}
+
+int rm_comm_info(const rm_ctx* c, int32_t* rank, int32_t* nranks, int32_t* ngpus) {
+  if (!c) return RM_ERR_INVALID;
+  if (rank) *rank = c->crank;
+  if (nranks) *nranks = c->subs.empty() ? c->cranks : (int32_t)c->subs.size();
+  if (ngpus) *ngpus = c->subs.empty() ? 1 : (int32_t)c->subs.size();
   return RM_OK;
 }
 

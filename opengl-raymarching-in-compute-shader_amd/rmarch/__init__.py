@@ -77,7 +77,8 @@ class rm_counters(C.Structure):
 class rm_config(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
                 ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
-                ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32)]
+                ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32),
+                ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
 class rm_camera_state(C.Structure):
@@ -199,7 +200,12 @@ _SIGS = {
                                      C.c_size_t, C.POINTER(C.c_size_t)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.POINTER(rm_uniforms)]),
+    "rm_comm_unique_id": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "rm_comm_init": (C.c_int, [_P, C.c_void_p, C.c_int32, C.c_int32]),
+    "rm_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                               C.POINTER(C.c_int32)]),
 }
+COMM_ID_BYTES = 128
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
 
@@ -369,17 +375,26 @@ class Renderer:
 
     def __init__(self, width: int, height: int, *, outputs: int = RM_OUT_RGBA8,
                  kernel: int = RM_KERNEL_AUTO, counters: bool = False, device: int = -1,
-                 row_block: int = 0, shard: int = 0, nshards: int = 1):
+                 row_block: int = 0, shard: int = 0, nshards: int = 1, ngpus: int = 0,
+                 devices: Optional[Sequence[int]] = None):
+        """ngpus >= 1: one context over ngpus devices (`devices`, or device,
+        device+1, ...), shards gathered with RCCL on the first (rm_config.ngpus)."""
+        devs = (C.c_int32 * len(devices))(*devices) if devices else None
+        if devices:
+            ngpus = len(devices)
         cfg = rm_config(width=width, height=height, device=device, outputs=outputs,
                         kernel=kernel, counters=1 if counters else 0, row_block=row_block,
-                        shard=shard, nshards=nshards)
+                        shard=shard, nshards=nshards, ngpus=ngpus,
+                        devices=C.cast(devs, C.POINTER(C.c_int32)) if devs else None)
         h = C.c_void_p()
         _check(lib().rm_create(C.byref(h), C.byref(cfg)))
         self._h = h
         self.width, self.height = width, height
         self.outputs = outputs if outputs else RM_OUT_RGBA8
         self.nshards, self.shard, self.row_block = max(nshards, 1), shard, row_block
-        self.rows = shard_rows_cap(height, row_block, nshards) if nshards > 1 else height
+        self.ngpus = ngpus
+        self.rows = (shard_rows_cap(height, row_block, nshards) if nshards > 1 and not ngpus
+                     else height)
 
     # -- lifetime
     def close(self) -> None:
@@ -519,6 +534,20 @@ class Renderer:
     def unshard_rgba8(self, gathered_ptr: int, frame_ptr: int) -> None:
         _check(lib().rm_unshard_rgba8(self._h, gathered_ptr, frame_ptr), self._h)
 
+    # -- one rank per process (rm_comm_init)
+    def comm_init(self, comm_id: bytes, nranks: int, rank: int) -> None:
+        """Join this shard context to an RCCL communicator: from then on dispatch
+        renders, gathers on rank 0 and (rank 0) assembles the full frame."""
+        buf = C.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
+        _check(lib().rm_comm_init(self._h, buf, nranks, rank), self._h)
+        if rank == 0:
+            self.rows = self.height
+
+    def comm_info(self) -> tuple:
+        r, n, g = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        _check(lib().rm_comm_info(self._h, C.byref(r), C.byref(n), C.byref(g)), self._h)
+        return r.value, n.value, g.value
+
     def enable_timing(self, on: bool = True) -> None:
         _check(lib().rm_enable_timing(self._h, int(on)), self._h)
 
@@ -527,6 +556,14 @@ class Renderer:
         n = C.c_int64(0)
         _check(lib().rm_kernel_time_ms(self._h, C.byref(ms), C.byref(n), int(reset)), self._h)
         return ms.value, n.value
+
+
+def comm_unique_id() -> bytes:
+    """An RCCL unique id (ncclGetUniqueId) for rm_comm_init; rank 0 creates it and
+    broadcasts it over the host's own channel."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().rm_comm_unique_id(buf, COMM_ID_BYTES))
+    return buf.raw
 
 
 # shader.hpp-style free functions over a Renderer ("program") ---------------------------

@@ -14,9 +14,13 @@
 // held = OR of W 1, A 2, S 4, D 8, ESC 16.  The loop stops after ESC, like
 // while (!glfwWindowShouldClose(window)) (main.cpp:92).
 //
+// --gpus N renders every frame on N GPUs of this node from this one process
+// (rm_config.ngpus: one row-block shard per device, RCCL gather onto the first,
+// SURVEY 8(e)); --graph replays each frame from captured hipGraphs.
+//
 //   rm_frameloop [--width W] [--height H] [--frames N] [--bounces B] [--aa 0|1]
 //                [--hard-shadows] [--kernel auto|pixel|wavequeue] [--dump out.ppm]
-//                [--input script.txt]
+//                [--input script.txt] [--gpus N] [--graph]
 #include <rm/camera.hpp>
 #include <rm/input.hpp>
 #include <rm/texture.hpp>
@@ -30,7 +34,7 @@
 
 int main(int argc, char** argv) {
   int W = 1080, H = 1080, frames = 120, bounce = 0, aa = 1, shadow = RM_SHADOW_SOFT;
-  int kernel = RM_KERNEL_AUTO;
+  int kernel = RM_KERNEL_AUTO, ngpus = 0, graph = 0;
   const char* dump = nullptr;
   const char* script = nullptr;
   for (int i = 1; i < argc; ++i) {
@@ -49,6 +53,8 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--hard-shadows")) shadow = RM_SHADOW_HARD;
     else if (!std::strcmp(argv[i], "--dump")) dump = next("--dump");
     else if (!std::strcmp(argv[i], "--input")) script = next("--input");
+    else if (!std::strcmp(argv[i], "--gpus")) ngpus = std::atoi(next("--gpus"));
+    else if (!std::strcmp(argv[i], "--graph")) graph = 1;
     else if (!std::strcmp(argv[i], "--kernel")) {
       std::string k = next("--kernel");
       kernel = k == "pixel" ? RM_KERNEL_PIXEL : k == "wavequeue" ? RM_KERNEL_WAVEQUEUE : RM_KERNEL_AUTO;
@@ -78,11 +84,15 @@ int main(int argc, char** argv) {
     camera.cameraPos = rm::vec3(0.0f, 0.0f, 15.0f);
   }
   rm::Texture tex(W, H);  // main.cpp:70-71
-  if (int rc = tex.GenerateTexture(RM_OUT_RGBA8, kernel); rc != RM_OK) {
+  if (int rc = tex.GenerateTexture(RM_OUT_RGBA8, kernel, -1, ngpus); rc != RM_OK) {
     std::fprintf(stderr, "GenerateTexture failed (%d): %s\n", rc, rm_last_error(nullptr));
     return 1;
   }
   rm_ctx* marching = tex.texOutput;
+  if (graph && rm_graph_enable(marching, 1) != RM_OK) {
+    std::fprintf(stderr, "rm_graph_enable failed: %s\n", rm_last_error(marching));
+    return 1;
+  }
   unsigned int workgroups = 39;  // main.cpp:76-77 (ignored by librm)
 
   using clk = std::chrono::steady_clock;
@@ -150,7 +160,8 @@ int main(int argc, char** argv) {
     rm::setVec2(marching, "iMouse", mu.iMouse[0], mu.iMouse[1]);
     rm::setInt(marching, "shadow_mode", shadow);
 
-    if (rm::dispatchCompute(marching) != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
+    const int drc = graph ? rm_graph_dispatch(marching) : rm::dispatchCompute(marching);
+    if (drc != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
       std::fprintf(stderr, "frame %d failed: %s\n", f, rm_last_error(marching));
       return 1;
     }
@@ -164,8 +175,9 @@ int main(int argc, char** argv) {
     }
   }
   const double secs = std::chrono::duration<double>(clk::now() - t0).count();
-  std::printf("frames %u  %.3f s  %.2f fps  %.2f Mpixels/s  (%dx%d, bounces %d, AA %d)\n", total,
-              secs, total / secs, total * (double)W * H / secs / 1e6, W, H, bounce, aa);
+  std::printf("frames %u  %.3f s  %.2f fps  %.2f Mpixels/s  (%dx%d, bounces %d, AA %d, gpus %d%s)\n",
+              total, secs, total / secs, total * (double)W * H / secs / 1e6, W, H, bounce, aa,
+              ngpus > 0 ? ngpus : 1, graph ? ", hipGraph" : "");
   if (dump) {
     std::vector<uint8_t> img((size_t)W * H * 4);
     if (rm_read_rgba8(marching, img.data(), 0, /*flip_y=*/1) != RM_OK) {

@@ -44,12 +44,60 @@ def test_structs_match_header_sizes(rm):
     assert C.sizeof(rm.rm_light) == 60
     assert C.sizeof(rm.rm_uniforms) == 64 + 60 + 4 * 5 + 12 + 8 + 4
     assert C.sizeof(rm.rm_counters) == 56
-    assert C.sizeof(rm.rm_config) == 36
+    assert C.sizeof(rm.rm_config) == 48  # 10 int32 + the devices pointer
     assert C.sizeof(rm.rm_camera_state) == 8 + 24 + 48
 
 
+def test_struct_layouts_match_the_c_compiler(rm, tmp_path):
+    """Every field offset of the ctypes mirrors equals the C compiler's for
+    include/rm_api.h (catches a field added on one side only)."""
+    import subprocess
+    structs = {"rm_config": rm.rm_config, "rm_uniforms": rm.rm_uniforms,
+               "rm_counters": rm.rm_counters, "rm_primitive": rm.rm_primitive,
+               "rm_camera_state": rm.rm_camera_state, "rm_input_state": rm.rm_input_state}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rm_api.h"', "int main(void) {"]
+    for name, py in structs.items():
+        lines.append(f'printf("{name} size %zu\\n", sizeof({name}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{name} {f} %zu\\n", offsetof({name}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for name, py in structs.items():
+        assert got[(name, "size")] == C.sizeof(py), name
+        for f, _ in py._fields_:
+            assert got[(name, f)] == getattr(py, f).offset, (name, f)
+
+
 def test_api_version(rm):
-    assert rm.lib().rm_api_version() == 1
+    assert rm.lib().rm_api_version() == 2
+
+
+def test_multi_gpu_config_validation_without_gpu(rm):
+    # RCCL-gathered frames are RGBA8 only, without counters; rejected before any device call
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(64, 64, ngpus=2, outputs=rm.RM_OUT_RGBA32F)
+    assert e.value.code == rm.RM_ERR_INVALID
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(64, 64, ngpus=2, counters=True)
+    assert e.value.code == rm.RM_ERR_INVALID
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(64, 64, ngpus=2, nshards=2, row_block=8)
+    assert e.value.code == rm.RM_ERR_INVALID
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(64, 64, ngpus=-1)
+    assert e.value.code == rm.RM_ERR_INVALID
+
+
+def test_comm_unique_id_without_gpu(rm):
+    """ncclGetUniqueId needs no device: rank 0 of a host without GPUs (a launcher)
+    can make the id; two calls give different ids."""
+    a, b = rm.comm_unique_id(), rm.comm_unique_id()
+    assert len(a) == rm.COMM_ID_BYTES and a != b
 
 
 def test_argument_validation_without_gpu(rm):

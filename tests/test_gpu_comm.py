@@ -1,0 +1,153 @@
+"""Multi-GPU frames behind the C-ABI: RCCL inside librm.
+
+Two forms, both replacing one reference dispatch (main.cpp:123-125) per frame:
+  * rm_config.ngpus: one process drives N devices (ncclCommInitAll), the frame is
+    assembled on the first;
+  * rm_comm_init: one rank per process (ncclCommInitRank), rank 0 assembles.
+This box has one GPU, so both run with a one-rank communicator: the render,
+the ncclGather (in place on rank 0), the k_unshard assembly and the captured
+hipGraph of all three run for real; only the number of peers is 1.  The
+N-rank shard geometry is covered by tests/test_gpu_api.py (shard assembly on
+one GPU, N in {2, 3, 8}) and tests/test_shard.py (gloo, world size 2).
+Every frame must equal a plain one-GPU render byte for byte.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _frames(rm, n, b=3, aa=True):
+    return [rm.sweep_uniforms(f, 120, b, aa, rm.RM_SHADOW_SOFT) for f in np.linspace(0, 119, n).astype(int)]
+
+
+def _reference(rm, W, H, us):
+    with rm.Renderer(W, H) as r:
+        out = []
+        for u in us:
+            r.dispatch(u)
+            out.append(r.read_rgba8())
+        return out
+
+
+@pytest.mark.parametrize("W,H,R", [(160, 90, 8), (37, 23, 4), (640, 360, 8)])
+def test_multi_gpu_context_one_device(rm, gpu, W, H, R):
+    us = _frames(rm, 4)
+    ref = _reference(rm, W, H, us)
+    with rm.Renderer(W, H, ngpus=1, row_block=R) as m:
+        assert m.comm_info() == (0, 1, 1)
+        for u, want in zip(us, ref):
+            m.dispatch(u)
+            np.testing.assert_array_equal(m.read_rgba8(), want)
+        # readback flip and graph replay work as on a one-GPU context
+        np.testing.assert_array_equal(m.read_rgba8(flip_y=True), ref[-1][::-1])
+        m.graph_enable(True)
+        for u, want in zip(us, ref):
+            m.graph_dispatch(u)
+            np.testing.assert_array_equal(m.read_rgba8(), want)
+
+
+def test_multi_gpu_context_explicit_device_list(rm, gpu):
+    us = _frames(rm, 2, b=1, aa=False)
+    ref = _reference(rm, 96, 64, us)
+    with rm.Renderer(96, 64, devices=[0]) as m:
+        for u, want in zip(us, ref):
+            m.dispatch(u)
+            np.testing.assert_array_equal(m.read_rgba8(), want)
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(96, 64, devices=[0, 0])
+    assert e.value.code == rm.RM_ERR_INVALID
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(96, 64, devices=[gpu])  # out of range
+    assert e.value.code == rm.RM_ERR_INVALID
+
+
+def test_multi_gpu_context_scene_table_and_external_output(rm, gpu):
+    import torch
+    W, H = 128, 72
+    u = _frames(rm, 1)[0]
+    ref = _reference(rm, W, H, [u])[0]
+    with rm.Renderer(W, H, ngpus=1) as m:
+        m.set_scene(rm.default_scene())  # the reference scene as a table: same image
+        assert len(m.get_scene()) == 6
+        m.dispatch(u)
+        np.testing.assert_array_equal(m.read_rgba8(), ref)
+        m.set_scene(None)
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        m.set_output_rgba8(out.data_ptr())
+        assert m.output_rgba8_ptr() == out.data_ptr()
+        m.dispatch(u)
+        m.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        with pytest.raises(rm.RMError):
+            m.set_stream(None)  # one stream per device, the context's own
+
+
+@pytest.mark.parametrize("W,H,R", [(160, 90, 8), (65, 3, 1)])
+def test_comm_rank_renders_gathers_and_assembles(rm, gpu, W, H, R):
+    us = _frames(rm, 4)
+    ref = _reference(rm, W, H, us)
+    with rm.Renderer(W, H, row_block=R, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        assert r.comm_info() == (0, 1, 1)
+        for u, want in zip(us, ref):
+            r.dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba8(), want)
+
+
+def test_comm_graph_captures_render_gather_and_assembly(rm, gpu):
+    """cfg 5's per-rank graph: render + ncclGather + k_unshard captured once and
+    replayed with new frame constants; a new output buffer re-captures."""
+    import torch
+    W, H = 192, 108
+    us = _frames(rm, 6)
+    ref = _reference(rm, W, H, us)
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        r.graph_enable(True)
+        for u, want in zip(us[:3], ref[:3]):  # the first runs eagerly (RCCL set-up), then replays
+            r.graph_dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba8(), want)
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(out.data_ptr())
+        for u, want in zip(us[3:], ref[3:]):
+            r.graph_dispatch(u)
+            r.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+def test_comm_init_validation(rm, gpu):
+    cid = rm.comm_unique_id()
+    with rm.Renderer(32, 32, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
+        with pytest.raises(rm.RMError) as e:  # RGBA8 only
+            r.comm_init(cid, 1, 0)
+        assert e.value.code == rm.RM_ERR_INVALID
+    with rm.Renderer(32, 32, row_block=8, shard=1, nshards=2) as r:
+        with pytest.raises(rm.RMError) as e:  # the shard must be the rank
+            r.comm_init(cid, 2, 0)
+        assert e.value.code == rm.RM_ERR_INVALID
+    with rm.Renderer(32, 32) as r:
+        r.comm_init(cid, 1, 0)
+        with pytest.raises(rm.RMError) as e:
+            r.comm_init(cid, 1, 0)
+        assert e.value.code == rm.RM_ERR_STATE
+
+
+def test_frameloop_on_a_multi_gpu_context(rm, gpu, tmp_path):
+    """The C++ host (rm_frameloop, the main.cpp:92-147 replacement) renders with
+    --gpus 1 (rm_config.ngpus, RCCL in librm, no torch) and with its graph, and
+    dumps the same last frame as a plain run."""
+    exe = os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd", "rm_frameloop")
+    base = [exe, "--width", "160", "--height", "96", "--frames", "5", "--bounces", "2"]
+    outs = {}
+    for name, extra in (("plain", []), ("gpus", ["--gpus", "1"]), ("graph", ["--gpus", "1", "--graph"])):
+        ppm = tmp_path / f"{name}.ppm"
+        p = subprocess.run(base + extra + ["--dump", str(ppm)], capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0, p.stderr
+        outs[name] = ppm.read_bytes()
+    assert outs["gpus"] == outs["plain"] and outs["graph"] == outs["plain"]

@@ -105,3 +105,38 @@ def test_gloo_gather_assembles_full_frame(rm, oracle):
         assert p.exitcode == 0
     full = oracle.render(rm.sweep_uniforms(40, 120, 2, True, 0), W, H)["rgba8"]
     np.testing.assert_array_equal(img, full)
+
+
+def _ids_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "opengl-raymarching-in-compute-shader_amd"))
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q.put((rank, bench.comm_ids(3, rank)))
+    dist.destroy_process_group()
+
+
+def test_bench_broadcasts_rccl_ids_over_gloo(rm):
+    """bench.py's N > 1 bootstrap (world size 2, gloo): rank 0 makes one RCCL id per
+    in-flight context (rm_comm_unique_id, no GPU needed) and every rank receives
+    the same ids in the same order, which rm_comm_init then joins."""
+    import multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ids_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1]
+    assert len(got[0]) == 3 and len(set(got[0])) == 3
+    assert all(len(i) == rm.COMM_ID_BYTES for i in got[0])
