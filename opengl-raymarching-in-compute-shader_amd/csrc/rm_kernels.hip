@@ -31,6 +31,12 @@
 #ifndef RM_ESC_SPLIT
 #define RM_ESC_SPLIT 1
 #endif
+#ifndef RM_ONE_EXIT
+#define RM_ONE_EXIT 1
+#endif
+#ifndef RM_MX_SPLIT
+#define RM_MX_SPLIT 1
+#endif
 #ifndef RM_CAP_EXIT
 #define RM_CAP_EXIT 1
 #endif
@@ -172,7 +178,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     //                <= ro.y + 5.5 <= tmax: no step ever escapes.
     // Only waves with a lane outside both cases run the loop with the test.
     const float QNAN = __builtin_nanf("");
-    auto run = [&](auto esc) {
+    auto run = [&](auto esc, auto usemx) {
       // The march runs in segments ending at the scalar step indices of the
       // step-cap check (RM_CAP_EXIT): the step loop itself is the plain one, with
       // the segment end as its scalar bound.  Between segments a lane's exit test
@@ -183,17 +189,40 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll 1
       for (;;) {
         if (live) {
+          if (RM_ONE_EXIT) {
+            // t advances on every step and the step's own t is kept in tp, so
+            // the loop has a single exit at its latch: hit | escape | proven miss
+            // (t + d past mx; a NaN fails the compare) | segment end.
+            float tp = t;
+            RM_UNROLL(RM_STEP_UNROLL)
+            for (int i = ib;; ++i) {
+              const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+              bool ex = d < 0.000001f * t;
+              dl = d;
+              tp = t;
+              t = t + d;
+              if (decltype(usemx)::value) ex = ex | !(t <= mx);
+              if (decltype(esc)::value) ex = ex | (d > tmax);
+              if (ex | (i >= iend)) break;
+            }
+            t = tp;
+          } else {
           RM_UNROLL(RM_STEP_UNROLL)
           for (int i = ib;; ++i) {
             const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
             const bool h = d < 0.000001f * t;
             dl = d;
             const float tn = t + d;
-            float probe = h ? QNAN : tn;
-            if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
-            if (!(probe <= mx)) break;
+            if (decltype(usemx)::value) {
+              float probe = h ? QNAN : tn;
+              if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
+              if (!(probe <= mx)) break;
+            } else if (h) {  // mx == +inf on every lane, no escape: the hit is the only exit
+              break;
+            }
             if (i >= iend) break;
             t = tn;
+          }
           }
         }
         if (iend >= nmax) break;
@@ -216,8 +245,11 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       }
     };
     const bool need_esc = (mx > tmax) && !(rd.y <= 0.0f && ro.y + 5.5f <= tmax);
-    if (!RM_ESC_SPLIT || __any(need_esc)) run(std::true_type());
-    else run(std::false_type());
+    // Waves of downward rays (rd.y <= 0: lin_exit_T gives mx = +inf, and no step
+    // escapes) leave on a hit only: the probe compare against mx is dropped.
+    if (!RM_ESC_SPLIT || __any(need_esc)) run(std::true_type(), std::true_type());
+    else if (RM_MX_SPLIT && !__any(!(mx == __builtin_huge_valf()))) run(std::false_type(), std::false_type());
+    else run(std::false_type(), std::true_type());
     asm volatile("" : "+v"(t), "+v"(dl));  // re-form the test, not a lane mask kept per step
     if (dl < 0.000001f * t) {
       const f3 q = add(ro, muls(rd, t));
@@ -441,7 +473,7 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
 
 // render glsl:218-251
 template <bool COUNT>
-__device__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+__device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   int id;
   f3 hcol;
@@ -587,11 +619,11 @@ static_assert(RM_STW == 4 || kSampleWaves == 1, "RM_STW != 4 needs one-wave work
 constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : RM_STW;
 constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : (kSampleWaves == 2 ? 4 : 16 / RM_STW);
 template <bool COUNT>
-__device__ __forceinline__ void sample_body(const Frame& F) {
+__device__ __forceinline__ void sample_body(const Frame& F, int bxi, int byi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s = lane & 3, q = lane >> 2;
-  const int by = tile_row(blockIdx.y, F.grid_y);
-  const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kSampleTileW * 4));
+  const int by = tile_row(byi, F.grid_y);
+  const int bx = tile_col(bxi, F.grid_x, 128 / (kSampleTileW * 4));
   const int px = kSampleWaves == 1 ? bx * kSampleTileW + q % RM_STW
                                    : bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
   const int lrow = kSampleWaves == 1 ? by * kSampleTileH + q / RM_STW
@@ -657,7 +689,7 @@ __global__ __launch_bounds__(RM_PIXEL_BLOCK, RM_PIXEL_MIN_WAVES) void k_pixel(Fr
 }
 template <bool COUNT>
 __global__ __launch_bounds__(RM_SAMPLE_BLOCK, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
-  sample_body<COUNT>(F);
+  sample_body<COUNT>(F, blockIdx.x, blockIdx.y);
 }
 
 // Step 0 of the primary rays, once per frame (see PrepSlot, rm_scene.hpp).

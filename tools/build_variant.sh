@@ -18,6 +18,7 @@ for f in rm_api rm_kernels rm_wavequeue rm_table; do
   /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/$f.hip" -o "$b/$f.o" &
 done
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
+[ -f "$src/$pkg/csrc/rm_comm.cpp" ] && { /opt/rocm/bin/hipcc $flags -x hip -c "$src/$pkg/csrc/rm_comm.cpp" -o "$b/rm_comm.o" & }
 if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed the table sources
   c=$src/$pkg/csrc
   python3 "$src/$pkg/tools/embed_sources.py" "$b/rm_jit_src.inc" rm_table.hip=$c/rm_table.hip \
@@ -26,6 +27,6 @@ if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed t
   /opt/rocm/bin/hipcc $flags -I"$b" -c "$c/rm_jit.hip" -o "$b/rm_jit.o" &
 fi
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o -lhiprtc
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o -lhiprtc -ldl
 rm -rf "$b"; [ "$src" != "$root" ] && rm -rf "$src"
 echo "$out/librm_$name.so"
