@@ -22,7 +22,7 @@ LIBRM    := $(PKG)/librm.so
 ORACLE   := oracle/_build/librm_oracle.so
 DRIVER   := $(PKG)/rm_frameloop
 
-RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_wavequeue.hip $(CSRC)/rm_table.hip $(CSRC)/rm_jit.hip $(CSRC)/rm_host.cpp $(CSRC)/rm_comm.cpp
+RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_table.hip $(CSRC)/rm_jit.hip $(CSRC)/rm_host.cpp $(CSRC)/rm_comm.cpp
 RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp $(CSRC)/rm_jit.hpp $(CSRC)/rm_comm.hpp include/rm_api.h
 # The table kernel's sources, embedded in librm.so for hiprtc (rm_jit.hip), under
 # the names they #include each other by.
@@ -57,7 +57,7 @@ $(PKG)/build/rm_comm.o: $(CSRC)/rm_comm.cpp $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_wavequeue.o $(PKG)/build/rm_table.o $(PKG)/build/rm_jit.o $(PKG)/build/rm_host.o $(PKG)/build/rm_comm.o
+$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_table.o $(PKG)/build/rm_jit.o $(PKG)/build/rm_host.o $(PKG)/build/rm_comm.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lhiprtc -ldl
 
 $(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h

@@ -203,8 +203,6 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="pixel", choices=["pixel", "wavequeue"],
-                    help="pixel = k_pixel (RM_KERNEL_AUTO's choice), wavequeue = k_wavequeue")
     ap.add_argument("--row-block", type=int, default=8,
                     help="rows per interleaved block when sharding over ranks")
     ap.add_argument("--graph", type=int, default=-1,
@@ -253,11 +251,8 @@ def main() -> int:
 
     cfg = CONFIGS[args.config]
     W, H = cfg["width"], cfg["height"]
-    kernel = rm.RM_KERNEL_WAVEQUEUE if args.kernel == "wavequeue" else rm.RM_KERNEL_PIXEL
+    kernel = rm.RM_KERNEL_PIXEL
     use_graph = (args.graph == 1) or (args.graph < 0 and args.config == 5)
-    if use_graph and kernel == rm.RM_KERNEL_WAVEQUEUE:
-        print("bench.py: --graph renders with the default kernel", file=sys.stderr)
-        return 2
     # Frames in flight: consecutive frames go to separate contexts, each with its own
     # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
     # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
@@ -386,7 +381,7 @@ def main() -> int:
             ops_total += algorithmic_ops(c)
             cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
     mean_kernel_ms = kernel_ms / max(launches, 1)
-    kname = ("k_sample" if cfg["aa"] else "k_pixel") if args.kernel == "pixel" else "k_wavequeue"
+    kname = "k_sample" if cfg["aa"] else "k_pixel"
     if scene is not None:
         kname = "k_table_sample" if cfg["aa"] else "k_table_pixel"
     pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}" + ("-spec" if spec else ""))

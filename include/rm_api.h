@@ -58,7 +58,6 @@ extern "C" {
 /* ---- kernel variants (rm_config.kernel) ----------------------------------- */
 #define RM_KERNEL_AUTO 0       /* the fastest measured variant: RM_KERNEL_PIXEL */
 #define RM_KERNEL_PIXEL 1      /* one thread per pixel, 8x8 pixel tile per wave, culled sdf */
-#define RM_KERNEL_WAVEQUEUE 2  /* persistent waves, per-lane job refill (ballot/popc) */
 
 /* Uniform block of computeShader.glsl:7,59-66.  vec4s carry w = 0
  * (main.cpp:103-106).  Layout is plain C, not std140. */
@@ -176,10 +175,6 @@ int rm_read_rgba8(rm_ctx *ctx, uint8_t *dst, size_t row_pitch, int flip_y);
 int rm_read_rgba32f(rm_ctx *ctx, float *dst, size_t row_pitch, int flip_y);
 /* Counters of the last dispatch (requires cfg.counters). */
 int rm_get_counters(rm_ctx *ctx, rm_counters *out);
-/* Diagnostic of the wave-queue kernel (requires cfg.counters): loop
- * iterations summed over all waves of the last dispatch.  SIMD utilisation of
- * the sdf loop = sdf evaluations / (64 * iterations).  0 for RM_KERNEL_PIXEL. */
-int rm_get_wave_iterations(rm_ctx *ctx, uint64_t *iters);
 /* Per-pixel sdf() evaluation counts of the last dispatch, summed over the
  * pixel's samples, reference units (requires cfg.counters). */
 int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
@@ -191,7 +186,7 @@ int rm_read_sdf_counts(rm_ctx *ctx, uint32_t *dst);
  * node's by-value argument (hipGraphExecKernelNodeSetParams) and replays the
  * graph on the context's stream (re-captured only when AA toggles, which
  * changes the grid and kernel).  Same kernel and image as rm_dispatch.
- * Not available with cfg.counters or RM_KERNEL_WAVEQUEUE. */
+ * Not available with cfg.counters. */
 int rm_graph_enable(rm_ctx *ctx, int enable);
 int rm_graph_dispatch(rm_ctx *ctx);
 
@@ -248,9 +243,15 @@ int rm_get_scene(const rm_ctx *ctx, rm_primitive *out, int32_t capacity, int32_t
  * RM_ERR_HIP with the compiler log in rm_last_error and leaves the scene as it
  * was.  enable == 0: the generic (LDS-staged) table kernel. */
 int rm_scene_specialize(rm_ctx *ctx, int enable);
+/* The register bound of the specialised table kernels in use: *waves = the
+ * waves per SIMD they were compiled for (8, 7 or 6: the most at which they need
+ * no scratch), or 0 when the generic table kernel (or the built-in scene)
+ * renders; a table that spills at 6 waves is not specialised. */
+int rm_scene_kernel_waves(const rm_ctx *ctx, int32_t *waves);
 /* Diagnostics: the code object rm_scene_specialize would load for this table
  * on `arch` (e.g. "gfx950"), compiled without a device.  *size = its size;
- * out == NULL queries the size only. */
+ * out == NULL queries the size only; *size = 0: the table is not specialised
+ * (see rm_scene_kernel_waves). */
 int rm_jit_code_object(const rm_primitive *prims, int32_t n, const char *arch, void *out,
                        size_t capacity, size_t *size);
 

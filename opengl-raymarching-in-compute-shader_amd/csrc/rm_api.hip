@@ -20,12 +20,9 @@
 #include "rm_scene.hpp"
 
 namespace rm {
-extern int g_wq_batch;
-extern int g_wq_blocks_per_cu;
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s);
-hipError_t launch_wavequeue(const rmd::Frame& F, bool counters, hipStream_t s, int num_cus);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s);
 }  // namespace rm
@@ -45,7 +42,6 @@ struct rm_ctx {
   rm_config cfg{};
   int device = 0;
   int rows = 0;  // rows rendered per dispatch (height, or the shard's rows_cap)
-  int num_cus = 256;
   rm_uniforms u{};
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -54,8 +50,6 @@ struct rm_ctx {
   float* d_rgba32f = nullptr;
   uint32_t* d_counts = nullptr;
   unsigned long long* d_counters = nullptr;
-  uint32_t* d_queue = nullptr;
-  float* d_prep = nullptr;        // k_prep's per-frame step-0 values (rm_scene.hpp PrepSlot)
   float* d_uv = nullptr;          // per-column / per-row uv table (Frame::uvx / uvy)
   uint32_t* d_scene = nullptr;    // runtime scene table (rm_set_scene), compiled words
   int nprims = 0;                 // 0: the built-in scene and its specialised kernel
@@ -139,8 +133,8 @@ int nccl_fail(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
   return fail(c, RM_ERR_HIP, std::string(what) + ": " + (r ? r->GetErrorString(e) : "RCCL"));
 }
 
-// Step 0 of every primary ray (rm_scene.hpp PrepSlot), on the host: what k_prep
-// computes, with the same IEEE operations in the same order (x86-64 SSE floats,
+// Step 0 of every primary ray (rm_scene.hpp PrepSlot), on the host: what the
+// render kernels' scene_lazy would compute at the camera, with the same IEEE operations in the same order (x86-64 SSE floats,
 // -ffp-contract=off), so d0 is bit-identical to the device's scene_exact at the
 // camera (sqrt_core / sqrt_cr_nonneg / div_capbb are the IEEE sqrt and divide on
 // the values reached here, rm_fastmath.hpp).  The bounds (slack, LB_k, b1, b2)
@@ -226,8 +220,6 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.rgba32f = (c->cfg.outputs & RM_OUT_RGBA32F) ? c->d_rgba32f : nullptr;
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
-  F.queue = c->d_queue;
-  F.prep = c->d_prep;
   prep_host(F.cam_pos, F.blend, F.omblend, F.prepv);
   F.scene = c->nprims ? reinterpret_cast<const float*>(c->d_scene) : nullptr;
   F.nprims = c->nprims;
@@ -262,8 +254,6 @@ void free_all(rm_ctx* c) {
   if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
   if (c->d_counts) (void)hipFree(c->d_counts);
   if (c->d_counters) (void)hipFree(c->d_counters);
-  if (c->d_queue) (void)hipFree(c->d_queue);
-  if (c->d_prep) (void)hipFree(c->d_prep);
   if (c->d_uv) (void)hipFree(c->d_uv);
   if (c->d_scene) (void)hipFree(c->d_scene);
   for (auto& p : c->ev_pool) {
@@ -276,8 +266,6 @@ void free_all(rm_ctx* c) {
   c->d_rgba32f = nullptr;
   c->d_counts = nullptr;
   c->d_counters = nullptr;
-  c->d_queue = nullptr;
-  c->d_prep = nullptr;
   c->d_uv = nullptr;
   c->d_scene = nullptr;
   c->stream = nullptr;
@@ -455,13 +443,13 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   if (cfg->ngpus < 0 || cfg->ngpus > 64)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: ngpus must be in 0..64");
   if (cfg->ngpus >= 1) {
-    if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_WAVEQUEUE)
+    if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_PIXEL)
       return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
     return create_multi(out, cfg);
   }
   if (cfg->outputs & ~(RM_OUT_RGBA8 | RM_OUT_RGBA32F))
     return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown output bits");
-  if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_WAVEQUEUE)
+  if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_PIXEL)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
   if (cfg->nshards > 1 &&
       (cfg->row_block <= 0 || cfg->shard < 0 || cfg->shard >= cfg->nshards))
@@ -497,9 +485,6 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     return code;
   };
   if ((rc = set_device(c)) != RM_OK) return bail(rc);
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
-    c->num_cus = prop.multiProcessorCount;
   rm_shard_rows_cap(c->cfg.height, c->cfg.row_block, c->cfg.nshards, &c->rows);
   const size_t npx = (size_t)c->rows * (size_t)c->cfg.width;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -522,8 +507,6 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     if ((e = hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess)
       return bail(hip_fail(c, e, "hipMalloc counters"));
   }
-  if ((e = hipMalloc(&c->d_queue, 256)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc queue"));
-  if ((e = hipMalloc(&c->d_prep, 64)) != hipSuccess) return bail(hip_fail(c, e, "hipMalloc prep"));
   {
     // uv of the pixel columns and rows with the shader's float operations
     // (glsl:301-305 and the cumulative sub-sample offsets of :309-332)
@@ -544,12 +527,8 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
         (e = hipMemcpy(c->d_uv, uv.data(), uv.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
       return bail(hip_fail(c, e, "uv table"));
   }
-  if ((e = hipMemsetAsync(c->d_prep, 0, 64, c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipMemset"));
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipStreamSynchronize"));
   rm_default_uniforms(&c->u);
-  // Tuning knobs of the wave-queue kernel; defaults are the tuned values.
-  if (const char* e = std::getenv("RM_WQ_BATCH")) rm::g_wq_batch = std::atoi(e);
-  if (const char* e = std::getenv("RM_WQ_BLOCKS_PER_CU")) rm::g_wq_blocks_per_cu = std::atoi(e);
   *out = c;
   return RM_OK;
 }
@@ -656,17 +635,11 @@ int render_launch(rm_ctx* c) {
   rmd::Frame F = make_frame(c);
   hipEvent_t e0, e1;
   if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
-  const int kernel = c->cfg.kernel == RM_KERNEL_AUTO ? RM_KERNEL_PIXEL : c->cfg.kernel;
-  if (kernel == RM_KERNEL_WAVEQUEUE) {
-    RM_HIP(c, hipMemsetAsync(c->d_queue, 0, 256, c->stream));
-  }
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
-  // a runtime scene table renders with the table kernel whatever the variant
+  // a runtime scene table renders with the table kernel
   hipError_t e = c->nprims ? (c->jit ? rm::launch_table_jit(c->jit, F, c->cfg.counters != 0, c->stream)
                                       : rm::launch_table(F, c->cfg.counters != 0, c->stream))
-                 : (kernel == RM_KERNEL_PIXEL)
-                     ? rm::launch_pixel(F, c->cfg.counters != 0, c->stream)
-                     : rm::launch_wavequeue(F, c->cfg.counters != 0, c->stream, c->num_cus);
+                           : rm::launch_pixel(F, c->cfg.counters != 0, c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
   c->dispatched = true;
@@ -795,19 +768,6 @@ int rm_get_counters(rm_ctx* c, rm_counters* out) {
   return RM_OK;
 }
 
-int rm_get_wave_iterations(rm_ctx* c, uint64_t* iters) {
-  if (!c || !iters) return RM_ERR_INVALID;
-  if (!c->cfg.counters) return fail(c, RM_ERR_STATE, "context created without counters");
-  if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
-  int rc = set_device(c);
-  if (rc != RM_OK) return rc;
-  unsigned long long h[8];
-  RM_HIP(c, hipStreamSynchronize(c->stream));
-  RM_HIP(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
-  *iters = h[6];
-  return RM_OK;
-}
-
 int rm_read_sdf_counts(rm_ctx* c, uint32_t* dst) {
   if (!c || !dst) return RM_ERR_INVALID;
   if (!c->cfg.counters) return fail(c, RM_ERR_STATE, "context created without counters");
@@ -890,8 +850,6 @@ int rm_graph_enable(rm_ctx* c, int enable) {
     return RM_OK;
   }
   if (c->cfg.counters) return fail(c, RM_ERR_STATE, "graph path does not collect counters");
-  if (c->cfg.kernel == RM_KERNEL_WAVEQUEUE)
-    return fail(c, RM_ERR_STATE, "graph path renders with the default kernel");
   c->graph_on = true;
   return RM_OK;
 }
@@ -965,6 +923,7 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
   if (c->specialize) {
     std::string err;
     if ((rc = rm::jit_table(words.data(), n, &jit, err)) != RM_OK) return fail(c, rc, err);
+    if (!jit->mod) jit = nullptr;  // no spill-free bound: the generic kernel
   }
   if (!c->d_scene) {
     RM_HIP(c, hipMalloc(&c->d_scene, rm::scene_words(RM_MAX_PRIMITIVES) * sizeof(uint32_t)));
@@ -1003,7 +962,14 @@ int rm_scene_specialize(rm_ctx* c, int enable) {
     c->specialize = false;
     return fail(c, rc, err);
   }
-  c->jit = jit;
+  c->jit = jit->mod ? jit : nullptr;  // no spill-free bound: the generic kernel
+  return RM_OK;
+}
+
+int rm_scene_kernel_waves(const rm_ctx* c, int32_t* waves) {
+  if (!c || !waves) return RM_ERR_INVALID;
+  const rm_ctx* r = c->subs.empty() ? c : c->subs[0];
+  *waves = r->jit ? r->jit->waves : 0;
   return RM_OK;
 }
 

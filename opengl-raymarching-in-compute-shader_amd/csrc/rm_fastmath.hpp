@@ -32,45 +32,17 @@ __device__ __forceinline__ float sqrt_core(float x) {
   return __builtin_fmaf(h, r, s);
 }
 
-// (RM_FAST_RCP, default off: measured no faster than the IEEE division here)
-// 1/x correctly rounded: v_rcp_f32 and one Newton step, proven bit-exact by
-// tools/exhaustive_fp.hip for every 2^-125 <= |x| <= 2^125; 0, inf, NaN and the
-// extreme magnitudes take the IEEE division (a rarely-taken branch).
-#ifndef RM_FAST_RCP
-#define RM_FAST_RCP 0
-#endif
-__device__ __forceinline__ float rcp_exact(float x) {
-  if (!RM_FAST_RCP) return 1.0f / x;
-  const float y = __builtin_amdgcn_rcpf(x);
-  const float e = __builtin_fmaf(-x, y, 1.0f);
-  float r = __builtin_fmaf(e, y, y);
-  const float ax = fabsf(x);
-  if (!(ax >= 0x1p-125f && ax <= 0x1p125f)) r = 1.0f / x;
-  return r;
-}
-
-// x / i for the bounce weights, i = 1..5 (glsl:186-187, i wave-uniform): powers
-// of two are exact multiplies; 3 and 5 use the Markstein sequence with the
-// correctly rounded reciprocal (as div_capbb), proven bit-exact over all finite
-// x, signed zeros included, by tools/exhaustive_fp.hip.  Other i (not reachable)
-// divide.
-__device__ __forceinline__ float div_small(float x, int i) {
-  if (!RM_FAST_RCP) return x / (float)i;
-  if (i == 1) return x;
-  if (i == 2) return x * 0.5f;
-  if (i == 4) return x * 0.25f;
-  if (i == 3 || i == 5) {
-    const float d = (float)i;
-    const float y = (i == 3) ? (1.0f / 3.0f) : (1.0f / 5.0f);
-    const float q = x * y;
-    const float r = __builtin_fmaf(-q, d, x);
-    return q == 0.0f ? q : __builtin_fmaf(r, y, q);  // keeps -0 / 3 == -0
-  }
-  return x / (float)i;
-}
+// 1/x and x / i (the bounce weights, i = 1..5, glsl:186-187) are IEEE
+// divisions: a v_rcp_f32 + Newton form (exact for 2^-125 <= |x| <= 2^125) and a
+// Markstein x/3, x/5 (exact over all finite x) were proven by
+// tools/exhaustive_fp.hip (profiles/r01_exhaustive_fp.log) but measured no
+// faster here than the division.
+__device__ __forceinline__ float rcp_exact(float x) { return 1.0f / x; }
+__device__ __forceinline__ float div_small(float x, int i) { return x / (float)i; }
 
 // 1/s for s = sqrt_cr_nonneg(d) of a finite d >= 0, i.e. s = 0 or
-// 2^-74.5 <= s <= 2^64, inside rcp_exact's proven range: no guard needed.  For
+// 2^-74.5 <= s <= 2^64, inside the v_rcp + Newton form's proven range
+// (tools/exhaustive_fp.hip): no guard needed.  For
 // s = 0 (and NaN) it gives NaN where the IEEE 1/s gives inf; normalize()
 // multiplies that by the zero vector, and 0 * inf is NaN too.
 __device__ __forceinline__ float rcp_of_sqrt(float s) {

@@ -14,9 +14,12 @@ struct Frame;
 namespace rm {
 
 // k_table_{pixel,sample}<counters> compiled for one table: fn[aa][counters].
+// waves == 0 (mod null): the table fits no spill-free register bound and renders
+// with the generic table kernel.
 struct JitTable {
   hipModule_t mod = nullptr;
   hipFunction_t fn[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  int waves = 0;  // the register bound compiled for (waves per SIMD, rm_jit.hip)
 };
 
 // Compiles (or finds in the process-wide cache) the table kernels for the

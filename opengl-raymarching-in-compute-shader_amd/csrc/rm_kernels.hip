@@ -1,97 +1,42 @@
 // rm_kernels.hip — the hot path: per-pixel SDF sphere tracing on gfx950.
 //
 // Reference: shaders/computeShader.glsl:68-344 (dispatched by main.cpp:123).
-// Two kernels compute the same pure function of (pixel, uniforms):
-//   * k_pixel      — one thread per pixel, structured control flow mirroring
-//                    the GLSL call tree (render -> bounce -> softshadow).  The
-//                    straightforward baseline and the debug-counter kernel.
-//   * k_wavequeue  — the performance kernel (rm_wavequeue.hip).
+// Two kernels compute the same pure function of (pixel, uniforms), with the
+// GLSL call tree (render -> bounce -> softshadow) as their control flow:
+//   * k_sample — 4x supersampled frames: one lane per (pixel, sample), a wave
+//                covers 4x4 pixels x 4 samples;
+//   * k_pixel  — frames without supersampling: one lane per pixel, 8x8 pixels
+//                per wave.
+// Each is built twice: COUNT = false is the production kernel (every
+// proof-based early exit taken), COUNT = true the counting build of the tests.
 // See DESIGN.md §4 for the kernel designs and their rooflines.
+//
+// Diagnostic builds only (tools/build_variant.sh; tests/test_abi.py compiles
+// them): RM_STATS (wave / lane counters, tools/stats_probe.py), RM_WAVE_TIMES
+// (per-wave lifetimes, tools/wave_timeline.hip), RM_DBL_<PHASE> (a phase run
+// twice: its marginal cost, tools/ab_kernel.py).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
 
 #include "rm_scene.hpp"
 
-#ifndef RM_LAZY_CULL
-#define RM_LAZY_CULL 1
-#endif
-#ifndef RM_SHADOW_EXIT
-#define RM_SHADOW_EXIT 1
-#endif
-#ifndef RM_MISS_EXIT
-#define RM_MISS_EXIT 1
-#endif
-#ifndef RM_PRIMARY_PREP
-#define RM_PRIMARY_PREP 1
-#endif
-#ifndef RM_MARCH_V2
-#define RM_MARCH_V2 1
-#endif
-#ifndef RM_ESC_SPLIT
-#define RM_ESC_SPLIT 1
-#endif
-#ifndef RM_ONE_EXIT
-#define RM_ONE_EXIT 1
-#endif
-#ifndef RM_MX_SPLIT
-#define RM_MX_SPLIT 1
-#endif
-#ifndef RM_CAP_EXIT
-#define RM_CAP_EXIT 1
-#endif
-#ifndef RM_CAP_I0
-#define RM_CAP_I0 16
-#endif
-#ifndef RM_CAP_REFL
-#define RM_CAP_REFL 0  // 1: the check in reflected marches too (5 VGPR spills, +24 MB scratch writes)
-#endif
-#ifndef RM_CAP_I1
-#define RM_CAP_I1 64
-#endif
-
-#ifndef RM_STEP_UNROLL
-#define RM_STEP_UNROLL 1
-#endif
-#define RM_STR_(x) #x
-#define RM_UNROLL(n) _Pragma(RM_STR_(unroll n))
-
 namespace rmd {
+
+// The primary march runs in segments ending at these scalar step indices, where
+// the lanes still marching take the step-cap miss check (rm_scene.hpp cap_miss).
+constexpr int kCapI0 = 16, kCapI1 = 64;
 
 #ifdef RM_WAVE_TIMES
 __device__ unsigned long long* g_wave_times;
-#endif
-#ifdef RM_PHASE_TIMING
-// Diagnostic build only: wave clock cycles spent per phase (tools/phase_probe.hip).
-// RM_PT(k, v) charges the time since the previous mark to phase k once v (the
-// phase's result) is computed; volatile asm keeps the marks in program order.
-__device__ unsigned long long g_phase[16];
-__device__ __forceinline__ unsigned long long pt_clock() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
-  return t;
-}
-#define RM_PT_BEGIN() unsigned long long pt_t0_ = pt_clock()
-#define RM_PT(k, v)                                                            \
-  do {                                                                         \
-    asm volatile("" ::"v"(v));                                                 \
-    const unsigned long long now_ = pt_clock();                                \
-    const unsigned long long m_ = __ballot(1);                                 \
-    if (__lane_id() == __builtin_ffsll(m_) - 1) atomicAdd(&g_phase[k], now_ - pt_t0_); \
-    pt_t0_ = pt_clock();                                                       \
-  } while (0)
-#else
-#define RM_PT_BEGIN() do {} while (0)
-#define RM_PT(k, v) do {} while (0)
 #endif
 
 struct Cnt {
   uint32_t rays, march, reflect, shadow, normals, lights;
 };
 
-// Cost probes (diagnostic builds only, tools/build_variant.sh): RM_DBL_<PHASE>
-// runs a phase twice on an opaque copy of its inputs and folds the copy in as
-// a no-op, so the time difference is that phase's marginal cost.
+// Keeps the compiler from hoisting a value (and its registers) across a loop,
+// and feeds the RM_DBL_<PHASE> cost probes an opaque copy of their inputs.
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -103,52 +48,47 @@ template <bool COUNT>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
                        float& dlast) {
   float t = 0.0f, dl = 0.0f;
-#if !RM_LAZY_CULL
-  int idl = 7;  // opU id of the last step's minimum
-#endif
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   bool hit = false;
-  // per-ray constants; the ro-dependent ones of primary rays come from k_prep
+  // per-ray constants; the ro-dependent ones of primary rays come from the host
+  // (rm_api.hip prep_host: every primary ray starts at the camera)
+  const bool prep = !reflected && F.prepv[PREP_VALID] != 0.0f;
   const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
   float s0, b1, b2;
-  if (RM_PRIMARY_PREP && !reflected && prep_at(F, PREP_VALID) != 0.0f) {
-    s0 = prep_at(F, PREP_SLACK);
-    b1 = prep_at(F, PREP_B1);
-    b2 = prep_at(F, PREP_B2);
+  if (prep) {
+    s0 = F.prepv[PREP_SLACK];
+    b1 = F.prepv[PREP_B1];
+    b2 = F.prepv[PREP_B2];
   } else {
     s0 = ray_s0(ro);
     lin_exit_b(ro, s0, 0.0f, b1, b2);
   }
-#if RM_LAZY_CULL
   LazyCull lc;
   lazy_init(lc, rd, rdl, s0, s1);
   // lin_exit's object bound T1 for the step-cap check, re-formed there from the
   // ray (rare) rather than kept live through the loop
-  // (opaque: keeps the compiler from hoisting it, and its registers, out of the loop)
   auto cap_T1 = [&](f3 o, f3 r) {
     float b1c, b2c;
-    if (RM_PRIMARY_PREP && !reflected && prep_at(F, PREP_VALID) != 0.0f) b1c = prep_at(F, PREP_B1);
+    if (prep) b1c = F.prepv[PREP_B1];
     else lin_exit_b(o, lc.s0, 0.0f, b1c, b2c);
     return lin_exit_T1(MISS_C, ray_rdl(r), lc.s1, b1c);
   };
-#endif
   // provable miss (rm_scene.hpp "early exits"): production stops there; the
   // counting build runs on to the reference's step count and poisons the colour
   // with NaN should the ray hit after all (parity tests compare NaN masks)
   const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
   bool proven_miss = false;
   int i0 = 1;
-#if RM_LAZY_CULL && RM_PRIMARY_PREP
-  // Primary rays: step 0 is at the camera for every pixel; k_prep evaluated it
+  // Primary rays: step 0 is at the camera for every pixel; the host evaluated it
   // once (its distance is exact, its bounds as the block would form them).
   // Each lane only turns the bounds into expiries with its own |rd|: the
   // re-test of scene_lazy with U = d0 (<= the block's running minimum).
-  if (!reflected && prep_at(F, PREP_VALID) != 0.0f) {
-    const float d0 = prep_at(F, PREP_D0), sl = prep_at(F, PREP_SLACK), pl = prep_at(F, PREP_PL);
+  if (prep) {
+    const float d0 = F.prepv[PREP_D0], sl = F.prepv[PREP_SLACK], pl = F.prepv[PREP_PL];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const float lb = prep_at(F, PREP_LB + k);
+      const float lb = F.prepv[PREP_LB + k];
       const float g = lb - d0 - sl;
       const float bud = __builtin_fmaxf(g * lc.inv2v, (lb - pl) * lc.invp);
       lc.te[k] = (g > 0.0f) ? 0.0f + bud : 0.0f;
@@ -159,17 +99,16 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     t = d0;
     i0 = 2;
   }
-#endif
-#if RM_MARCH_V2 && RM_LAZY_CULL && RM_MISS_EXIT && !defined(RM_STATS)
+#ifndef RM_STATS
   if (!COUNT) {
-    // Production loop.  A lane leaves on hit | escape | proven miss, folded by
-    // VALU selects into one compare (a NaN probe fails `<=`, so does a finite
-    // t + d past the exit threshold; mx may be +inf); the 512 / 256 step cap is
-    // the same step for every lane of the wave (all start at i0), so it is a
-    // scalar loop bound.  t advances only when the lane goes on, so at the exit
-    // (t, dl) is the last step's pair and `dl < 1e-6 t` re-forms its hit test
-    // exactly.  A NaN distance (degenerate scenes) leaves at once: the
-    // reference marches on with t = NaN to the cap, also a miss.
+    // Production loop.  A lane leaves on hit | escape | proven miss; the 512 /
+    // 256 step cap is the same step for every lane of the wave (all start at
+    // i0), so it is a scalar loop bound.  t advances on every step and the
+    // step's own t is kept in tp, so the loop has a single exit at its latch
+    // (hit | escape | t + d past mx, a NaN failing the compare | segment end)
+    // and at the exit (t, dl) is the last step's pair: `dl < 1e-6 t` re-forms
+    // its hit test exactly.  A NaN distance (degenerate scenes) leaves at once:
+    // the reference marches on with t = NaN to the cap, also a miss.
     //
     // The escape test d > tmax is implied, for a lane, by either of
     //   mx <= tmax:  d > tmax  =>  t + d >= d > tmax >= mx (t >= 0, rounding is
@@ -177,56 +116,34 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     //   rd.y <= 0 and ro.y + 5.5 <= tmax:  d <= plane(t) = (ro.y + rd.y t) + 5.5
     //                <= ro.y + 5.5 <= tmax: no step ever escapes.
     // Only waves with a lane outside both cases run the loop with the test.
+    // Waves of downward rays only (rd.y <= 0 gives mx = +inf) also drop the mx
+    // compare: the hit is their only lane exit.
     const float QNAN = __builtin_nanf("");
     auto run = [&](auto esc, auto usemx) {
-      // The march runs in segments ending at the scalar step indices of the
-      // step-cap check (RM_CAP_EXIT): the step loop itself is the plain one, with
-      // the segment end as its scalar bound.  Between segments a lane's exit test
-      // is re-formed from its last (t, dl) (same operations, same result), the
-      // lanes still marching take the check, and those that go on take the step.
-      int ib = i0, iend = (RM_CAP_EXIT && (RM_CAP_REFL || !reflected)) ? RM_CAP_I0 : nmax;
+      // The primary march runs in segments ending at kCapI0 and kCapI1: the step
+      // loop itself is the plain one, with the segment end as its scalar bound.
+      // Between segments a lane's exit test is re-formed from its last (t, dl)
+      // (same operations, same result), the lanes still marching take the
+      // step-cap check, and those that go on take the step.
+      int ib = i0, iend = !reflected ? kCapI0 : nmax;
       bool live = true;
 #pragma unroll 1
       for (;;) {
         if (live) {
-          if (RM_ONE_EXIT) {
-            // t advances on every step and the step's own t is kept in tp, so
-            // the loop has a single exit at its latch: hit | escape | proven miss
-            // (t + d past mx; a NaN fails the compare) | segment end.
-            float tp = t;
-            RM_UNROLL(RM_STEP_UNROLL)
-            for (int i = ib;; ++i) {
-              const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-              bool ex = d < 0.000001f * t;
-              dl = d;
-              tp = t;
-              t = t + d;
-              if (decltype(usemx)::value) ex = ex | !(t <= mx);
-              if (decltype(esc)::value) ex = ex | (d > tmax);
-              if (ex | (i >= iend)) break;
-            }
-            t = tp;
-          } else {
-          RM_UNROLL(RM_STEP_UNROLL)
+          float tp = t;
           for (int i = ib;; ++i) {
             const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-            const bool h = d < 0.000001f * t;
+            bool ex = d < 0.000001f * t;
             dl = d;
-            const float tn = t + d;
-            if (decltype(usemx)::value) {
-              float probe = h ? QNAN : tn;
-              if (decltype(esc)::value) probe = (d > tmax) ? QNAN : probe;
-              if (!(probe <= mx)) break;
-            } else if (h) {  // mx == +inf on every lane, no escape: the hit is the only exit
-              break;
-            }
-            if (i >= iend) break;
-            t = tn;
+            tp = t;
+            t = t + d;
+            if (decltype(usemx)::value) ex = ex | !(t <= mx);
+            if (decltype(esc)::value) ex = ex | (d > tmax);
+            if (ex | (i >= iend)) break;
           }
-          }
+          t = tp;
         }
         if (iend >= nmax) break;
-#if RM_CAP_EXIT
         {
           float probe = (dl < 0.000001f * t) ? QNAN : t + dl;
           if (decltype(esc)::value) probe = (dl > tmax) ? QNAN : probe;
@@ -239,16 +156,13 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
           }
           if (live) t = probe;
         }
-#endif
         ib = iend + 1;
-        iend = iend < RM_CAP_I1 ? RM_CAP_I1 : nmax;  // segments end at I0 < I1 < nmax
+        iend = iend < kCapI1 ? kCapI1 : nmax;  // segments end at I0 < I1 < nmax
       }
     };
     const bool need_esc = (mx > tmax) && !(rd.y <= 0.0f && ro.y + 5.5f <= tmax);
-    // Waves of downward rays (rd.y <= 0: lin_exit_T gives mx = +inf, and no step
-    // escapes) leave on a hit only: the probe compare against mx is dropped.
-    if (!RM_ESC_SPLIT || __any(need_esc)) run(std::true_type(), std::true_type());
-    else if (RM_MX_SPLIT && !__any(!(mx == __builtin_huge_valf()))) run(std::false_type(), std::false_type());
+    if (__any(need_esc)) run(std::true_type(), std::true_type());
+    else if (!__any(!(mx == __builtin_huge_valf()))) run(std::false_type(), std::false_type());
     else run(std::false_type(), std::true_type());
     asm volatile("" : "+v"(t), "+v"(dl));  // re-form the test, not a lane mask kept per step
     if (dl < 0.000001f * t) {
@@ -263,8 +177,8 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     return -1.0f;
   }
 #endif
-  // One exit per step (hit | escape | step cap | proven miss), tested with
-  // VALU: a single exec-mask update per iteration.
+  // Counting build (and RM_STATS): one exit per step (hit | escape | step cap
+  // | proven miss); the proofs are only checked.
 #ifdef RM_STATS
   int nst = 0;  // this lane's steps (diagnostic builds)
 #endif
@@ -280,11 +194,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
       }
     }
 #endif
-#if RM_LAZY_CULL
     const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-#else
-    const float d = scene<true>(add(ro, muls(rd, t)), F.blend, F.omblend, idl);
-#endif
     if (COUNT) {
       if (reflected) c.reflect++;
       else c.march++;
@@ -292,19 +202,15 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     hit = d < 0.000001f * t;
     dl = d;
     bool stop = hit | (d > tmax) | (i >= nmax);
-#if RM_CAP_EXIT && RM_LAZY_CULL && RM_MISS_EXIT
-    if (i == RM_CAP_I0 || i == RM_CAP_I1) {  // same check as the production loop
+    if (!reflected && (i == kCapI0 || i == kCapI1)) {  // same check as the production loop
       const bool cm = !stop && cap_miss(t, d, nmax - i, ro.y, rd.y, cap_T1(ro, rd));
       if (COUNT) proven_miss |= cm;
       else stop |= cm;
     }
-#endif
     t += stop ? 0.0f : d;  // t >= +0: t + 0 == t
-    if (RM_MISS_EXIT) {
-      const bool gone = !stop && lin_exit(mx, t);
-      if (COUNT) proven_miss |= gone;
-      else stop |= gone;
-    }
+    const bool gone = !stop && lin_exit(mx, t);
+    if (COUNT) proven_miss |= gone;
+    else stop |= gone;
     if (stop) break;
   }
 #ifdef RM_STATS
@@ -316,11 +222,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   if (hit) {
     // the opU id (and colour) of the hit: from the last step's sdf (same point)
     const f3 q = add(ro, muls(rd, t));
-#if RM_LAZY_CULL
     id = lazy_id(lc, t);
-#else
-    id = idl;
-#endif
     col = hit_color(id, q);
     if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
     dlast = dl;
@@ -331,22 +233,10 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   return -1.0f;
 }
 
-// GetNormal glsl:278-288
 // GetNormal glsl:278-288, samples with shared culling (rm_scene.hpp).  HAVE_C0:
 // the centre sample sdf(pos) is the primary march's last distance (same point).
-#ifndef RM_NORMAL_INLINE
-#define RM_NORMAL_INLINE 0
-#endif
 template <bool COUNT, bool HAVE_C0>
-#if RM_NORMAL_INLINE
-__device__ __forceinline__
-#else
-__device__
-#endif
-f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
-#ifdef RM_ABL_NO_NORMAL
-  return mk(0.0f, 1.0f, 0.0f);
-#endif
+__device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
   if (COUNT) c.normals++;
   float vx, vy, vz;
   normal_samples<HAVE_C0>(pos, F.blend, F.omblend, c0, vx, vy, vz);
@@ -372,18 +262,15 @@ __device__ __forceinline__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c
 }
 template <bool COUNT>
 __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c) {
-#ifdef RM_ABL_NO_SHADOW
-  return 1.0f;
-#endif
   float res = 1.0f, t = 0.0f;
   int dummy;
   const float ex = shadow_exit_init(F.k, ro, rd);
   for (int i = 0; i < 16; ++i) {
-    if (RM_SHADOW_EXIT && lin_exit(ex, t)) {  // the remaining steps are no-ops
+    if (lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;
       return res;
     }
-    float h = scene<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
+    float h = scene_cull<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
     RM_STAT(2);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
@@ -392,22 +279,6 @@ __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, C
   }
   return res;
 }
-
-// RM_LDS_STASH: the bounce loop's colour state and hit point are parked in LDS
-// across each reflected march (volatile accesses: the values leave the VGPRs),
-// so the march has the 64-VGPR budget to itself.  One-wave workgroups: 64 lanes
-// x 9 floats = 2.3 KB per workgroup.
-#ifndef RM_LDS_STASH
-#define RM_LDS_STASH 0
-#endif
-#if RM_LDS_STASH
-// (plain LDS accesses with a compiler memory barrier between the stores and the
-// loads: volatile ones would lose the LDS address space and go through flat)
-__device__ __forceinline__ float* stash_slot() {
-  __shared__ float stash[9 * 64];
-  return stash + (threadIdx.x & 63);
-}
-#endif
 
 // bounce glsl:163-199 (dead tail skipped; see rm_oracle.h "live" counters)
 template <bool COUNT>
@@ -420,25 +291,11 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     // After a MATTE prevObject every remaining iteration is a colour no-op
     // (glsl:181,189-190): stop instead of running the dead marches.
     if (prevMatte) break;
-    RM_PT_BEGIN();
     rayDir = reflect(rayDir, normal);
     int id;
     f3 tcol;
     float dl;
-#if RM_LDS_STASH
-    float* sv = stash_slot();
-    const f3 ro_b = add(pos, muls(normal, 0.001f));
-    sv[0] = color.x; sv[64] = color.y; sv[128] = color.z;
-    sv[192] = prevColor.x; sv[256] = prevColor.y; sv[320] = prevColor.z;
-    sv[384] = pos.x; sv[448] = pos.y; sv[512] = pos.z;
-    asm volatile("" ::: "memory");  // the loads below re-read LDS: the values leave the VGPRs
-    float th = march<COUNT>(F, ro_b, rayDir, true, id, tcol, c, dl);
-    color = mk(sv[0], sv[64], sv[128]);
-    prevColor = mk(sv[192], sv[256], sv[320]);
-    pos = mk(sv[384], sv[448], sv[512]);
-#else
     float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c, dl);
-#endif
 #ifdef RM_DBL_BMARCH
     if (!COUNT) {
       int id2; f3 tc2; float dl2;
@@ -446,24 +303,20 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
       th = (th2 == th) ? th : __builtin_nanf("");
     }
 #endif
-    RM_PT(4, th);
     pos = add(pos, muls(rayDir, th));
     // The normal of a miss on the last bounce is never read: skip it.
     // (the hit point is pos + rayDir t, not the march's ro + rd t: no centre reuse)
     if (th != -1.0f || i < F.bounces) normal = get_normal<COUNT, false>(F, pos, c);
-    RM_PT(5, normal.x);
     if (th == -1.0f) {
       tcol = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
     } else {
       if (COUNT) c.lights++;
       tcol = point_light(F, tcol, normal, pos);
     }
-    RM_PT(6, tcol.x);
     if (id == 7 && !prevMatte && i < 3) {
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
       color = muls(color, div_small(sh, i));
     }
-    RM_PT(7, color.x);
     color = add(color, divi(mul(tcol, prevColor), i));
     prevColor = tcol;
     prevMatte = (id == 7);  // material of the hit: MATTE only for the floor; dummy is 1.0
@@ -477,7 +330,6 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   int id;
   f3 hcol;
-  RM_PT_BEGIN();
   float dl;
   float th = march<COUNT>(F, ro, rd, false, id, hcol, c, dl);
 #ifdef RM_DBL_MARCH
@@ -487,11 +339,9 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     th = (th2 == th) ? th : __builtin_nanf("");
   }
 #endif
-  RM_PT(0, th);
   if (th != -1.0f) {
     f3 pos = add(ro, muls(rd, th));
     f3 normal = get_normal<COUNT, true>(F, pos, c, dl);
-    RM_PT(1, normal.x);
     if (COUNT) c.lights++;
     color = point_light(F, hcol, normal, pos);
 #ifdef RM_DBL_LIGHT
@@ -500,12 +350,10 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
       color = mk(vmin(color.x, c2.x), vmin(color.y, c2.y), vmin(color.z, c2.z));
     }
 #endif
-    RM_PT(2, color.x);
     if (id == 7) {
       f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
       color = muls(color, sh);
-      RM_PT(3, color.x);
       return gamma(color);
     }
     if (F.bounces > 0) color = bounce<COUNT>(F, rd, pos, normal, color, hcol, c);
@@ -521,34 +369,20 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 
 // tile_row / tile_col (dispatch order): rm_scene.hpp
 
-// main glsl:291-344, one thread per pixel.  A 256-thread workgroup covers a
-// 16x16 pixel tile and each wave an 8x8 sub-tile, so the 64 rays of a wave
-// are spatially coherent (similar step counts, same culled primitives).
-// Workgroup of RM_PIXEL_BLOCK threads = 1, 2 or 4 waves of 8x8 pixels.  One-wave
-// workgroups keep the CUs fuller: a finished wave's slot is refilled at once
-// instead of waiting for its workgroup's slowest wave.
-#ifndef RM_PIXEL_BLOCK
-#define RM_PIXEL_BLOCK 64
-#endif
-constexpr int kPixelWaves = RM_PIXEL_BLOCK / 64;
-constexpr int kTileW = kPixelWaves >= 2 ? 16 : 8;
-constexpr int kTileH = kPixelWaves == 4 ? 16 : 8;
-#ifndef RM_PIXEL_AA
-#define RM_PIXEL_AA 0
-#endif
-#ifndef RM_PIXEL_MIN_WAVES
-#define RM_PIXEL_MIN_WAVES 8
-#endif
-#ifndef RM_SAMPLE_MIN_WAVES
-#define RM_SAMPLE_MIN_WAVES 8
-#endif
+// main glsl:291-344, one thread per pixel, frames without supersampling (AA
+// frames go to k_sample).  One-wave workgroups of an 8x8 pixel tile: the 64
+// rays of a wave are spatially coherent (similar step counts, same culled
+// primitives), and a finished wave's slot is refilled at once instead of
+// waiting for its workgroup's slowest wave.  This replaces the reference's
+// 39x39 tiles; its W/wg truncation band (main.cpp:123) is not reproduced.
+constexpr int kTileW = 8, kTileH = 8;
 template <bool COUNT>
 __device__ __forceinline__ void pixel_body(const Frame& F) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const int by = tile_row(blockIdx.y, F.grid_y);
   const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kTileW * 4));
-  const int px = bx * kTileW + (wave & 1) * 8 + (lane & 7);
-  const int lrow = by * kTileH + (wave >> 1) * 8 + (lane >> 3);
+  const int px = bx * kTileW + (lane & 7);
+  const int lrow = by * kTileH + (lane >> 3);
   if (px >= F.width || lrow >= F.rows) return;
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
@@ -556,32 +390,13 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
   float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
   if (py >= 0) {
     f3 ro, rd;
-    // launch_pixel sends AA frames to k_sample: k_pixel's own 4-sample loop is
-    // compiled only with RM_PIXEL_AA=1 (its accumulators cost registers)
-    if (RM_PIXEL_AA && F.aa) {
-#pragma unroll 1
-      for (int s = 0; s < 4; ++s) {
-        const float x = F.uvx[px * 5 + 1 + s], y = F.uvy[py * 5 + 1 + s];
-        cast_ray(F, x, y, ro, rd);
-        if (COUNT) c.rays++;
-        f3 col = render<COUNT>(F, ro, rd, c);
-        o0 += col.x;
-        o1 += col.y;
-        o2 += col.z;
-      }
-      o0 = o0 / 4.0f;
-      o1 = o1 / 4.0f;
-      o2 = o2 / 4.0f;
-      o3 = 1.0f;
-    } else {
-      cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
-      if (COUNT) c.rays++;
-      f3 col = render<COUNT>(F, ro, rd, c);
-      o0 = col.x;
-      o1 = col.y;
-      o2 = col.z;
-      o3 = 1.0f;
-    }
+    cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
+    if (COUNT) c.rays++;
+    f3 col = render<COUNT>(F, ro, rd, c);
+    o0 = col.x;
+    o1 = col.y;
+    o2 = col.z;
+    o3 = 1.0f;
   }
   store_pixel(F, idx, o0, o1, o2, o3);
   if (COUNT) {
@@ -596,44 +411,27 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
 }
 
 // main glsl:291-344 with 4x supersampling, one thread per (pixel, sample).
-// The 4 samples of a pixel sit in 4 adjacent lanes, so a wave covers a 4x4
-// pixel tile with all its samples (the most coherent 64 rays available: the
-// sample rays of one pixel are sub-pixel apart).  Lane s re-forms the
-// cumulative uv of glsl:311-332 with the same sequential float adds, and lane
+// The 4 samples of a pixel sit in 4 adjacent lanes, so a one-wave workgroup
+// covers a 4x4 pixel tile with all its samples (the most coherent 64 rays
+// available: the sample rays of one pixel are sub-pixel apart; 8x2 and 16x1
+// tiles measured 3 % and 17 % slower).  Lane s reads the cumulative uv of
+// glsl:311-332 from the host tables (the same sequential float adds), and lane
 // s == 0 sums the samples in the reference's fixed order ((c0+c1)+c2)+c3 via
 // lane shuffles before the /4 (glsl:315-335).
-// Workgroup of RM_SAMPLE_BLOCK threads = 1, 2 or 4 waves of 4x4 pixels x 4 samples
-// (one-wave workgroups by default, as for k_pixel: 7 % faster than four).
-#ifndef RM_SAMPLE_BLOCK
-#define RM_SAMPLE_BLOCK 64
-#endif
-constexpr int kSampleWaves = RM_SAMPLE_BLOCK / 64;
-#if RM_LDS_STASH
-static_assert(RM_SAMPLE_BLOCK == 64 && RM_PIXEL_BLOCK == 64, "the LDS stash is sized for one-wave workgroups");
-#endif
-// RM_STW: pixel columns of a one-wave tile (4: 4x4 pixels, 8: 8x2, 16: 16x1)
-#ifndef RM_STW
-#define RM_STW 4
-#endif
-static_assert(RM_STW == 4 || kSampleWaves == 1, "RM_STW != 4 needs one-wave workgroups");
-constexpr int kSampleTileW = kSampleWaves >= 2 ? 8 : RM_STW;
-constexpr int kSampleTileH = kSampleWaves == 4 ? 8 : (kSampleWaves == 2 ? 4 : 16 / RM_STW);
+constexpr int kSampleTileW = 4, kSampleTileH = 4;
 template <bool COUNT>
-__device__ __forceinline__ void sample_body(const Frame& F, int bxi, int byi) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void sample_body(const Frame& F) {
+  const int lane = threadIdx.x & 63;
   const int s = lane & 3, q = lane >> 2;
-  const int by = tile_row(byi, F.grid_y);
-  const int bx = tile_col(bxi, F.grid_x, 128 / (kSampleTileW * 4));
-  const int px = kSampleWaves == 1 ? bx * kSampleTileW + q % RM_STW
-                                   : bx * kSampleTileW + (wave & 1) * 4 + (q & 3);
-  const int lrow = kSampleWaves == 1 ? by * kSampleTileH + q / RM_STW
-                                     : by * kSampleTileH + (wave >> 1) * 4 + (q >> 2);
+  const int by = tile_row(blockIdx.y, F.grid_y);
+  const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kSampleTileW * 4));
+  const int px = bx * kSampleTileW + q % kSampleTileW;
+  const int lrow = by * kSampleTileH + q / kSampleTileW;
   if (px >= F.width || lrow >= F.rows) return;  // all 4 lanes of a pixel leave together
   const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
   Cnt c = {0, 0, 0, 0, 0, 0};
   f3 col = mk(0.0f, 0.0f, 0.0f);
-  RM_PT_BEGIN();
 #ifdef RM_WAVE_TIMES
   const unsigned long long wt0 = wall_clock64();
 #endif
@@ -657,7 +455,6 @@ __device__ __forceinline__ void sample_body(const Frame& F, int bxi, int byi) {
     atomicAdd(&F.counters[4], (unsigned long long)c.normals);
     atomicAdd(&F.counters[5], (unsigned long long)c.lights);
   }
-  RM_PT(8, col.x);
 #ifdef RM_WAVE_TIMES
   // diagnostic (tools/wave_timeline.hip): per-wave start/end and hardware slot
   if (lane == 0) {
@@ -680,52 +477,23 @@ __device__ __forceinline__ void sample_body(const Frame& F, int bxi, int byi) {
   if (COUNT) F.sdf_counts[idx] = cnt;
 }
 
-// Entry points: frame constants by value (kernel arguments, rm_dispatch) or
-// through a device pointer (graph replay, rm_graph_dispatch: the graph copies
-// the per-frame constants from pinned host memory before the launch).
+// Entry points: the frame constants by value (kernel arguments in SGPRs).
+// 64 VGPRs: 8 waves per SIMD, the most a SIMD holds (the kernels are latency
+// bound; 7 and 6 waves measured slower).
 template <bool COUNT>
-__global__ __launch_bounds__(RM_PIXEL_BLOCK, RM_PIXEL_MIN_WAVES) void k_pixel(Frame F) {
+__global__ __launch_bounds__(64, 8) void k_pixel(Frame F) {
   pixel_body<COUNT>(F);
 }
 template <bool COUNT>
-__global__ __launch_bounds__(RM_SAMPLE_BLOCK, RM_SAMPLE_MIN_WAVES) void k_sample(Frame F) {
-  sample_body<COUNT>(F, blockIdx.x, blockIdx.y);
-}
-
-// Step 0 of the primary rays, once per frame (see PrepSlot, rm_scene.hpp).
-// The same device code as scene_lazy's first step at p = camera: the
-// distance is scene_exact's value (the exact minimum), the bounds are the
-// re-test's fma(v_sqrt(|p - c|^2), LO, -(ABS + R)).
-__global__ __launch_bounds__(64) void k_prep(Frame F) {
-  if (threadIdx.x != 0) return;
-  const f3 p = mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2]);
-  int id;
-  const float d0 = scene_exact<true>(p, F.blend, F.omblend, id);
-  const Offs o = offsets(p);
-  const float sl = ray_s0(p);
-  const float tz = p.z - 10.0f;
-  const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-  const float x[5] = {(o.ax * o.ax + o.ay2) + o.az2, (o.bx * o.bx + o.ay2) + o.az2,
-                      (o.cx2 + o.ay2) + o.az2, (o.cx2 + o.ay2) + tz * tz,
-                      (kx * kx + ky * ky) + kz * kz};
-  const float R[5] = {3.0f, 3.0f, R_BLEND_LO, R_TORUS, R_CAPSULE};
-  float* out = const_cast<float*>(F.prep);
-  out[PREP_VALID] = (d0 > 0.0f && d0 <= 400.0f) ? 1.0f : 0.0f;
-  out[PREP_D0] = d0;
-  out[PREP_SLACK] = sl;
-  out[PREP_PL] = (p.y + 5.5f) + sl;
-  float b1, b2;
-  lin_exit_b(p, sl, 0.0f, b1, b2);
-  out[PREP_B1] = b1;
-  out[PREP_B2] = b2;
-  for (int k = 0; k < 5; ++k)
-    out[PREP_LB + k] = __builtin_fmaf(__builtin_amdgcn_sqrtf(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+__global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
+  sample_body<COUNT>(F);
 }
 
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
 // One grid row per frame row: the source row (shard, local row) is computed once
 // per workgroup in scalar registers; lanes copy 16 B (4 pixels) each when rows
-// are 16-B aligned (width % 4 == 0), one pixel otherwise.
+// are 16-B aligned (width % 4 == 0 and both images 16-B aligned), one pixel
+// otherwise.
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
@@ -761,19 +529,18 @@ void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy) {
 // kernels read the grid from their arguments, not from the hidden dispatch
 // arguments, so the prologue's tile arithmetic waits for one round of loads.
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
-  if (!RM_PREP_HOST) hipLaunchKernelGGL(rmd::k_prep, dim3(1), dim3(64), 0, s, F);
   const dim3 grid(F.grid_x, F.grid_y);
   if (F.aa) {
     if (counters)
-      hipLaunchKernelGGL(rmd::k_sample<true>, grid, dim3(RM_SAMPLE_BLOCK), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<true>, grid, dim3(64), 0, s, F);
     else
-      hipLaunchKernelGGL(rmd::k_sample<false>, grid, dim3(RM_SAMPLE_BLOCK), 0, s, F);
+      hipLaunchKernelGGL(rmd::k_sample<false>, grid, dim3(64), 0, s, F);
     return hipGetLastError();
   }
   if (counters)
-    hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(64), 0, s, F);
   else
-    hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(RM_PIXEL_BLOCK), 0, s, F);
+    hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(64), 0, s, F);
   return hipGetLastError();
 }
 
@@ -791,7 +558,10 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s) {
-  const bool vec = width % 4 == 0;
+  // 16-B copies need 16-B rows (width % 4 == 0) and 16-B aligned images: the
+  // C-ABI takes caller pointers, which may be offset
+  const bool vec = width % 4 == 0 && ((reinterpret_cast<uintptr_t>(gathered) |
+                                       reinterpret_cast<uintptr_t>(frame)) % 16 == 0);
   const unsigned per_row = (unsigned)(vec ? width / 4 : width);
   const dim3 grid((per_row + 255) / 256, (unsigned)(height < 65535 ? height : 65535));
   const uint32_t* g = static_cast<const uint32_t*>(gathered);

@@ -93,10 +93,7 @@ struct Frame {
   float* rgba32f;        // [rows][width][4] or null
   uint32_t* sdf_counts;  // [rows][width] or null (counter builds)
   unsigned long long* counters;  // 6 x u64 (counter builds)
-  uint32_t* queue;       // work-queue head (wave-queue kernel), zeroed per dispatch
-  const float* prep;     // step 0 of the primary rays (PrepSlot), written by k_prep
-                         // (RM_PREP_HOST=0 builds only)
-  float prepv[12];       // the same values by value, from the host (RM_PREP_HOST, default)
+  float prepv[12];       // step 0 of the primary rays (PrepSlot), from the host per frame
   const float* scene;    // runtime scene table (rm_set_scene), TABLE_WORDS per primitive, or null
   int32_t nprims;        // entries in `scene`
   int32_t grid_x, grid_y;  // k_pixel / k_sample grid (rm::pixel_grid): ordinary kernel
@@ -107,7 +104,7 @@ struct Frame {
 // Three exact evaluations of the same sdf (value and opU id equal to a literal
 // transcription):
 //   scene_exact  — every primitive;
-//   scene_cull   — bounding-sphere culling (shadow march, normal probes, wave-queue);
+//   scene_cull   — bounding-sphere culling (shadow march, normal probes);
 //   scene_lazy   — lazy culling along a march ray (RayMarch / reflectedRay loops).
 // opU (glsl:105): a later primitive replaces the running one unless the
 // running distance is strictly smaller, so ties go to the later primitive.
@@ -388,38 +385,22 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
 //   t_j < t_i + (LB_k - plane(p_i) - slack) / (|rd| + rd.y) * (1 - 2^-10)
 // (|rd| + rd.y >= 0; level and downward rays get 2x and more).  te_k is the
 // later of the two expiries; both are valid, so their max is.
-// Third budget, for a primitive the ray moves away from (RM_DIR_BUDGET).
-// f(t) = |p(t) - c| is convex along the ray, so f(t_j) >= f(t_i) + f'(t_i)(t_j - t_i)
-// with f'(t_i) = rd.(p_i - c) / |p_i - c|.  When rd.(p_i - c) >= 0 (checked with
-// a 2 |rd| slack margin, far above the float error of p_i and of the dot), LB_k
-// does not decrease from t_i on, and the gap closes at |rd| + s1 at most (the
-// minimum's growth and the slack's) instead of 2 |rd| + s1:
-//   te_k = t_i + (LB_k - U_i - slack) / |rd| * (1 - 2^-10);
-// against the plane, at rd.y + s1 instead of |rd| + rd.y, and never when
-// rd.y + s1 <= 0 (a downward ray past a primitive never re-tests it again):
-//   te_k = t_i + (LB_k - plane(p_i) - slack) / (rd.y + s1) * (1 - 2^-10).
-#ifndef RM_DIR_BUDGET
-#define RM_DIR_BUDGET 0  // measured slower (cfg3 +8.5 %, plane term alone +7 %): off
-#endif
-#ifndef RM_DIR_G
-#define RM_DIR_G 1  // 0: only the plane term uses the direction (A/B)
-#endif
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
   float s0, s1;  // slack(t) = s0 + s1 t >= 2^-14 (|ro|_1 + |rd| t + 64)  (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
-#if RM_DIR_BUDGET
-  float invq;    // (1 - 2^-10) / (rd.y + s1) (rounded down), or 2^100 when rd.y + s1 <= 0
-#endif
   float tb;      // t of the last step that entered the re-test block
   int idb;       // the opU id found there
 };
 
 // Step 0 of every primary ray is the same computation: castRay starts all of
-// them at the camera (glsl:68-74) and p(0) = ro + rd*0 = ro exactly.  k_prep
-// runs it once per frame and leaves these values for the render kernel:
+// them at the camera (glsl:68-74) and p(0) = ro + rd*0 = ro exactly.  The host
+// forms it once per frame (rm_api.hip prep_host, the same IEEE operations; the
+// bounds only need to be valid, and the IEEE sqrt is within the 2^-12 margins
+// made for v_sqrt) and passes these values by value in Frame::prepv, so the
+// render kernel's prologue has no dependent load:
 enum PrepSlot : int {
   PREP_VALID = 0,   // 1 when 0 < d0 <= 400 (no hit or escape at step 0)
   PREP_D0 = 1,      // sdf(camera), the step-0 distance (exact, same ops as scene_lazy)
@@ -430,17 +411,6 @@ enum PrepSlot : int {
   PREP_B2 = 10,
   PREP_COUNT = 11
 };
-// RM_PREP_HOST (default): the host forms these per frame (rm_api.hip prep_host,
-// the same IEEE operations; the bounds only need to be valid, and the IEEE sqrt
-// is within the 2^-12 margins made for v_sqrt) and passes them by value, so the
-// render kernel's prologue has no dependent load and no k_prep launch precedes it.
-#ifndef RM_PREP_HOST
-#define RM_PREP_HOST 1
-#endif
-__device__ __forceinline__ float prep_at(const Frame& F, int k) {
-  return RM_PREP_HOST ? F.prepv[k] : F.prep[k];
-}
-
 // Per-ray constants shared by the lazy culler and the linear exits: |rd| from
 // one v_sqrt (within 1.5 ulp) and the slack line s0 + s1 t, rounded up with
 // 2^-12 margins: s0 >= 2^-14 (|ro|_1 + 64), s1 >= 2^-14 |rd|.
@@ -464,44 +434,16 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
-#if RM_DIR_BUDGET
-  // rd.y + s1 rounds within 2^-24 of the exact sum; v_rcp within 1 ulp
-  const float q = rd.y + s1;
-  c.invq = q > 0.0f ? (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(q) * (1.0f - 0x1p-16f) : 0x1p100f;
-#endif
   c.s0 = s0;
   c.s1 = s1;
   c.tb = -1.0f;
   c.idb = 7;
 }
 
-// RM_LAZY_WAVE: the block and each re-test are entered per wave (any lane
-// expired) and every active lane re-tests: lanes whose te has not expired keep
-// max(te, new te) -- both expiries are valid -- so the idle lanes of a
-// divergent re-test extend their budgets for free.
-#ifndef RM_LAZY_WAVE
-#define RM_LAZY_WAVE 1
-#endif
-#ifndef RM_LAZY_ALL
-#define RM_LAZY_ALL 0
-#endif
-#ifndef RM_TE_FMA
-#define RM_TE_FMA 1
-#endif
-#ifndef RM_LAZY_EXACT_TE
-#define RM_LAZY_EXACT_TE 0
-#endif
-#if RM_LAZY_ALL
-#define RM_LZ_ANY(c) true
-#define RM_LZ_BLOCK(c) __any(c)
-#elif RM_LAZY_WAVE
-#define RM_LZ_ANY(c) __any(c)
-#define RM_LZ_BLOCK(c) __any(c)
-#else
-#define RM_LZ_ANY(c) (c)
-#define RM_LZ_BLOCK(c) (c)
-#endif
-
+// The block and each re-test are entered per wave (any lane expired) and every
+// active lane re-tests: lanes whose te has not expired keep max(te, new te) --
+// both expiries are valid -- so the idle lanes of a divergent re-test extend
+// their budgets for free.
 // The opU id of the minimum (glsl:105,110-121), as scene_exact<true> gives it,
 // is lazy_id(): the primitives are taken in the reference's order with ties
 // going to the later one, the plane last; culled primitives are strictly above
@@ -515,7 +457,7 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
   const float py = ro.y + rd.y * t;
   float m = py + 5.5f;  // plane, exact (glsl:85,121); running minimum
   RM_STAT(8);
-  if (RM_LZ_BLOCK(t >= lc.temin)) {
+  if (__any(t >= lc.temin)) {
     const float plane = m;
     float mp = __builtin_huge_valf();  // minimum over the evaluated primitives
     int idp = 7;
@@ -524,19 +466,13 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     const float slack = __builtin_fmaf(lc.s1, t, lc.s0);
     const float inv2v = lc.inv2v, invp = lc.invp;
     const float pl = m + slack;  // plane(p_i) + slack
-    // an exactly evaluated k: its value bounds it like LB does (RM_LAZY_EXACT_TE),
-    // so a k that is not the minimum gets a budget instead of a re-test next step
-    auto take = [&](float v, int k, float& te) {
-      if (RM_LAZY_EXACT_TE) {
-        const float g = v - m - slack;
-        if (g > 0.0f) te = t + __builtin_fmaxf(g * inv2v, (v - pl) * invp);
-      }
+    auto take = [&](float v, int k) {
       idp = (v <= mp) ? k : idp;
       mp = vmin(mp, v);
       m = vmin(m, v);
     };
     // re-test k; returns true when k must be evaluated exactly at this step
-    auto retest = [&](float x, float R, float& te, int k, float nd) -> bool {
+    auto retest = [&](float x, float R, float& te, int k) -> bool {
       RM_STAT(1);
       RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
@@ -546,61 +482,46 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       // expired lane and the idle one.  t + max(b1, b2, 0) == max(t + b1, t + b2, t)
       // (rounding is monotone); the fmas round once instead of twice, inside the
       // budgets' 2^-10 margin.
-#if RM_DIR_BUDGET
-      // nd = rd.(p - c_k): nd * inv2v >= slack  =>  nd >= 2 |rd| slack (inv2v <= 1/(2|rd|))
-      const bool away = nd * inv2v >= slack;
-      const float tn = vmax3(__builtin_fmaf((RM_DIR_G && away) ? g + g : g, inv2v, t),
-                             __builtin_fmaf(lb - pl, away ? lc.invq : invp, t), t);
-      const bool expired = t >= te;
-      te = te_max(te, tn);
-#elif RM_TE_FMA
       const float tn = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), t);
       const bool expired = t >= te;
       te = te_max(te, tn);
-#else
-      const float bud = __builtin_fmaxf(__builtin_fmaxf(g * inv2v, (lb - pl) * invp), 0.0f);
-      const bool expired = t >= te;
-      te = __builtin_fmaxf(te, t + bud);
-#endif
       return expired & !(g > 0.0f);
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
-    if (RM_LZ_ANY(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
+    if (__any(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
-      if (retest(x0, 3.0f, lc.te[0], 0, (rd.x * o.ax + rd.y * o.ay) + rd.z * o.az)) {
+      if (retest(x0, 3.0f, lc.te[0], 0)) {
         RM_STAT(10);
-        take(sqrt_core(x0) - 3.0f, 0, lc.te[0]);
+        take(sqrt_core(x0) - 3.0f, 0);
       }
     }
-    if (RM_LZ_ANY(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
+    if (__any(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
-      if (retest(x1, 3.0f, lc.te[1], 1, (rd.x * o.bx + rd.y * o.ay) + rd.z * o.az)) {
+      if (retest(x1, 3.0f, lc.te[1], 1)) {
         RM_STAT(11);
-        take(sqrt_core(x1) - 3.0f, 1, lc.te[1]);
+        take(sqrt_core(x1) - 3.0f, 1);
       }
     }
-    if (RM_LZ_ANY(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
+    if (__any(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
-      if (retest(xs, R_BLEND_LO, lc.te[2], 2, (rd.x * o.cx + rd.y * o.ay) + rd.z * o.az)) {
+      if (retest(xs, R_BLEND_LO, lc.te[2], 2)) {
         RM_STAT(12);
-        take(sd_blend(o, xs, blend, omblend), 4, lc.te[2]);
+        take(sd_blend(o, xs, blend, omblend), 4);
       }
     }
-    if (RM_LZ_ANY(t >= lc.te[3])) {  // torus, glsl:119
+    if (__any(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3,
-                 (rd.x * o.cx + rd.y * o.ay) + rd.z * tz)) {
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
         RM_STAT(13);
-        take(sd_torus(o, tz), 5, lc.te[3]);
+        take(sd_torus(o, tz), 5);
       }
     }
-    if (RM_LZ_ANY(t >= lc.te[4])) {  // capsule, glsl:120
+    if (__any(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4,
-                 (rd.x * kx + rd.y * ky) + rd.z * kz)) {
+      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4)) {
         RM_STAT(14);
-        take(sd_capsule(o, p), 6, lc.te[4]);
+        take(sd_capsule(o, p), 6);
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
@@ -610,16 +531,6 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
   return m;
 }
 __device__ __forceinline__ int lazy_id(const LazyCull& lc, float t) { return lc.tb == t ? lc.idb : 7; }
-
-#ifndef RM_SCENE_CULL
-#define RM_SCENE_CULL 1
-#endif
-
-template <bool WANT_ID>
-__device__ __forceinline__ float scene(f3 p, float blend, float omblend, int& id) {
-  return RM_SCENE_CULL ? scene_cull<WANT_ID>(p, blend, omblend, id)
-                       : scene_exact<WANT_ID>(p, blend, omblend, id);
-}
 
 // ---- provable early exits (softshadow, misses) ---------------------------------------
 // With C, R_ALL a sphere enclosing all five bounded primitives and
@@ -766,20 +677,13 @@ __device__ __forceinline__ f3 hit_color(int id, f3 p) {
 // (GLSL 4.50 §8.2; the GL drivers the reference runs on evaluate it this way),
 // on the hardware transcendentals v_log_f32 / v_exp_f32.  pow(0, y) = 0.  Its
 // difference to a correctly rounded pow is a few float ulps (measured in
-// tests/test_gpu_parity.py); RM_POW_OCML selects ocml's powf instead.
-#ifndef RM_POW_OCML
-#define RM_POW_OCML 0
-#endif
+// tests/test_gpu_parity.py, tools/pow_error.py).
 __device__ __forceinline__ float gpow(float x, float y) {
-  if (RM_POW_OCML) return powf(x, y);
   return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 }
 
 // getPointLight glsl:253-276
 __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f3 pos) {
-#ifdef RM_ABL_NO_LIGHT
-  return color;
-#endif
   f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
   f3 ambient = mk(F.lamb[0], F.lamb[1], F.lamb[2]);
   f3 viewDir = normalize(sub(pos, mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2])));
@@ -798,9 +702,6 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
 }
 
 __device__ __forceinline__ f3 gamma(f3 c) {
-#ifdef RM_ABL_NO_GAMMA
-  return c;
-#endif
   return mk(gpow(c.x, 0.4545f), gpow(c.y, 0.4545f), gpow(c.z, 0.4545f));
 }
 
@@ -821,22 +722,15 @@ __device__ __forceinline__ uint32_t quantize(float c) {
   return (uint32_t)(v * 255.0f + 0.5f);
 }
 
-// Dispatch order of the tile rows (RM_ROW_ORDER): 0 natural (bottom up),
-// 1 top down, 2 inside out (middle row first, then alternately below and above).
-// The slowest waves (rays grazing the floor near the horizon, silhouettes) sit
-// in the middle band of an upright view; started first they no longer form a
-// tail behind the cheap sky and near-floor rows (cfg3 1.24 -> 1.18 ms).
-#ifndef RM_ROW_ORDER
-#define RM_ROW_ORDER 2
-#endif
+// Dispatch order of the tile rows: inside out (the middle row first, then
+// alternately below and above).  The slowest waves (rays grazing the floor near
+// the horizon, silhouettes) sit in the middle band of an upright view; started
+// first they no longer form a tail behind the cheap sky and near-floor rows
+// (cfg3 1.24 -> 1.18 ms against the natural order).
 __device__ __forceinline__ int tile_row(int b, int n) {
-  if (RM_ROW_ORDER == 1) return n - 1 - b;
-  if (RM_ROW_ORDER == 2) {
-    // mid, mid-1, mid+1, mid-2, ...: b < n covers [mid - n/2, mid + (n-1)/2] = [0, n-1]
-    const int mid = n / 2, k = (b + 1) >> 1;
-    return (b & 1) ? mid - k : mid + k;
-  }
-  return b;
+  // mid, mid-1, mid+1, mid-2, ...: b < n covers [mid - n/2, mid + (n-1)/2] = [0, n-1]
+  const int mid = n / 2, k = (b + 1) >> 1;
+  return (b & 1) ? mid - k : mid + k;
 }
 
 // XCD-aware tile column: one-wave workgroups go round-robin to the 8 XCDs

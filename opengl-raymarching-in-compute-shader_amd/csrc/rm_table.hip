@@ -45,9 +45,6 @@
 #define RM_TS_INLINE
 #endif
 
-#ifndef RM_TABLE_LDS
-#define RM_TABLE_LDS 1  // 0: read the table through the scalar cache instead of LDS
-#endif
 
 namespace rmd {
 
@@ -57,20 +54,10 @@ struct TCnt {
 
 using rm::TABLE_WORDS;
 
-#ifndef RM_TABLE_CULL
-#define RM_TABLE_CULL 1
-#endif
-#ifndef RM_TABLE_LAZY
-#define RM_TABLE_LAZY 1
-#endif
-#ifndef RM_TABLE_FAST_SQRT
-#define RM_TABLE_FAST_SQRT 1
-#endif
 // Correctly rounded sqrt of a sum of squares (x >= 0, +inf or NaN).  The fast
 // form is sqrt_cr_nonneg (exact on [0, FLT_MAX], rm_fastmath.hpp) with +inf
 // passed through, so it equals the IEEE sqrt on the whole domain.
 __device__ __forceinline__ float isqrt_ieee(float x) {
-  if (!RM_TABLE_FAST_SQRT) return __builtin_sqrtf(x);
   const float s = sqrt_cr_nonneg(x);
   return x == __builtin_inff() ? x : s;
 }
@@ -127,7 +114,7 @@ struct Table {
   }
   // sdf(p).hitpoint and the index of the opU winner.
   //
-  // Culling (RM_TABLE_CULL): an entry whose lower bound at p exceeds an upper
+  // Culling: an entry whose lower bound at p exceeds an upper
   // bound U of the final minimum is strictly above that minimum, so it can
   // neither be the opU winner nor tie it (ties go to the later entry) and
   // skipping it leaves (d, best) unchanged.  U = min(running minimum, the
@@ -141,7 +128,7 @@ struct Table {
   __device__ __forceinline__ float dist(f3 p, int& best) const {
     const float INF = __builtin_huge_valf();
     float U = INF, slack = 0.0f;
-    if (RM_TABLE_CULL) {
+    {
       RM_TS_UNROLL
       for (int k = 0; k < n; ++k)
         if (type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(entry(k), RM_PRIM_PLANE, p, blend, omblend));
@@ -155,7 +142,7 @@ struct Table {
     for (int k = 0; k < n; ++k) {
       const float* P = entry(k);
       // (spheres: the exact value costs no more than the bound)
-      if (RM_TABLE_CULL && P[rm::TW_BALL + 3] != INF && type(k) != RM_PRIM_SPHERE) {
+      if (P[rm::TW_BALL + 3] != INF && type(k) != RM_PRIM_SPHERE) {
         const float bx = p.x - P[rm::TW_BALL], by = p.y - P[rm::TW_BALL + 1], bz = p.z - P[rm::TW_BALL + 2];
         const float x = (bx * bx + by * by) + bz * bz;
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), 1.0f - 0x1p-12f, -(P[rm::TW_BALL + 3] + slack));
@@ -202,9 +189,6 @@ struct Table {
   __device__ __forceinline__ float material(int k) const { return entry(k)[rm::TW_MATERIAL]; }
 };
 
-#ifndef RM_TABLE_EXITS
-#define RM_TABLE_EXITS 1
-#endif
 // Provable early exits for any table (the generic form of rm_scene.hpp's
 // lin_exit_T; bounds from rm::exit_bounds, rm_host.cpp).  Every entry's float
 // value at p(t) = ro + rd t is at least
@@ -222,7 +206,7 @@ struct Table {
 // as in lin_exit_T.
 __device__ __forceinline__ float table_exit_T(const float* ex, float c, float hmin, f3 ro, f3 rd) {
   const float INF = __builtin_huge_valf();
-  if (!RM_TABLE_EXITS || ex[rm::EX_VALID] == 0.0f) return INF;
+  if (ex[rm::EX_VALID] == 0.0f) return INF;
   const float HI = 1.0f + 0x1p-12f, LO = 1.0f - 0x1p-12f;
   const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
   const float sig = ex[rm::EX_SIGMA];
@@ -253,7 +237,7 @@ __device__ __forceinline__ float table_exit_T(const float* ex, float c, float hm
   return T;
 }
 
-// Lazy culling along a march (RM_TABLE_LAZY; the generic form of scene_lazy,
+// Lazy culling along a march (the generic form of scene_lazy,
 // rm_scene.hpp) for p(t) = ro + rd t with t growing by the returned distance
 // after every step (tmarch, tshadow).  Slot j tracks entry k_j (rm::exit_bounds)
 // with an expiry te[j] before which k_j is proven strictly above the minimum.
@@ -280,7 +264,7 @@ struct TLazy {
   __device__ __forceinline__ TLazy(const Table& S, f3 ro, f3 rd) {
     const float INF = __builtin_huge_valf();
     ex = S.exits();
-    ns = RM_TABLE_LAZY ? (int)ex[rm::EX_NSLOTS] : 0;
+    ns = (int)ex[rm::EX_NSLOTS];
     const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
     always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
 #pragma unroll
@@ -471,13 +455,11 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   return S;
 #else
   S.n = F.nprims;
-  if (RM_TABLE_LDS) {
-    for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
-    __syncthreads();
-    S.t = lds;
-  } else {
-    S.t = F.scene;
-  }
+  // staged in LDS: every entry read is a broadcast (the scalar cache measured
+  // 1-4 % slower)
+  for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
+  __syncthreads();
+  S.t = lds;
   return S;
 #endif
 }
@@ -492,16 +474,12 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 }
 
 // Waves per SIMD the register allocation must allow.  The per-table specialised
-// kernels at 8 waves (64 VGPRs) spill a little (~40 MB of scratch traffic per cfg3
-// launch, PMC) and are still faster: table-spec 2.27 -> 2.10 ms per frame (7 waves:
-// 2.16).  The generic kernel (91 VGPRs unbounded, 5 waves) is fastest bounded to
-// 6 waves (80 VGPRs, 8 spills): table 3.87 -> 3.47 ms per frame.
+// kernels (RM_TABLE_STATIC) get the bound from rm_jit.hip: the most waves at
+// which the table's code needs no scratch.  The generic kernel (91 VGPRs
+// unbounded, 5 waves) is fastest bounded to 6 waves (80 VGPRs, 8 spills):
+// table 3.87 -> 3.47 ms per frame.
 #ifndef RM_TABLE_MIN_WAVES
-#ifdef RM_TABLE_STATIC
-#define RM_TABLE_MIN_WAVES 8
-#else
 #define RM_TABLE_MIN_WAVES 6
-#endif
 #endif
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
@@ -582,7 +560,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F
 namespace rm {
 
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s) {
-  const size_t lds = RM_TABLE_LDS ? rm::scene_words(F.nprims) * sizeof(float) : 0;
+  const size_t lds = rm::scene_words(F.nprims) * sizeof(float);
   if (F.aa) {
     const dim3 g((F.width + 3) / 4, (F.rows + 3) / 4);
     if (counters)

@@ -37,7 +37,6 @@ RM_SHADOW_SOFT = 0
 RM_SHADOW_HARD = 1
 RM_KERNEL_AUTO = 0
 RM_KERNEL_PIXEL = 1
-RM_KERNEL_WAVEQUEUE = 2
 
 
 class RMError(RuntimeError):
@@ -164,7 +163,6 @@ _SIGS = {
     "rm_read_rgba32f": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
     "rm_get_counters": (C.c_int, [_P, C.POINTER(rm_counters)]),
     "rm_read_sdf_counts": (C.c_int, [_P, _P]),
-    "rm_get_wave_iterations": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "rm_graph_enable": (C.c_int, [_P, C.c_int]),
     "rm_graph_dispatch": (C.c_int, [_P]),
     "rm_set_stream": (C.c_int, [_P, _P]),
@@ -196,6 +194,7 @@ _SIGS = {
     "rm_set_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32]),
     "rm_get_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
     "rm_scene_specialize": (C.c_int, [_P, C.c_int]),
+    "rm_scene_kernel_waves": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "rm_jit_code_object": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.c_char_p, C.c_void_p,
                                      C.c_size_t, C.POINTER(C.c_size_t)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
@@ -459,6 +458,13 @@ class Renderer:
         """Render tables with kernels compiled for the table (hiprtc; rm_scene_specialize)."""
         _check(lib().rm_scene_specialize(self.handle, int(on)), self.handle)
 
+    def scene_kernel_waves(self) -> int:
+        """Waves per SIMD of the specialised table kernels in use (rm_scene_kernel_waves);
+        0 = the generic table kernel or the built-in scene."""
+        w = C.c_int32(0)
+        _check(lib().rm_scene_kernel_waves(self.handle, C.byref(w)), self.handle)
+        return int(w.value)
+
     def get_scene(self) -> list:
         n = C.c_int32(0)
         out = (rm_primitive * RM_MAX_PRIMITIVES)()
@@ -508,11 +514,6 @@ class Renderer:
         c = rm_counters()
         _check(lib().rm_get_counters(self._h, C.byref(c)), self._h)
         return c.as_dict()
-
-    def wave_iterations(self) -> int:
-        v = C.c_uint64(0)
-        _check(lib().rm_get_wave_iterations(self._h, C.byref(v)), self._h)
-        return int(v.value)
 
     def sdf_counts(self) -> np.ndarray:
         out = np.empty((self.rows, self.width), np.uint32)

@@ -19,7 +19,7 @@
 // SURVEY 8(e)); --graph replays each frame from captured hipGraphs.
 //
 //   rm_frameloop [--width W] [--height H] [--frames N] [--bounces B] [--aa 0|1]
-//                [--hard-shadows] [--kernel auto|pixel|wavequeue] [--dump out.ppm]
+//                [--hard-shadows] [--kernel auto|pixel] [--dump out.ppm]
 //                [--input script.txt] [--gpus N] [--graph]
 #include <rm/camera.hpp>
 #include <rm/input.hpp>
@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--graph")) graph = 1;
     else if (!std::strcmp(argv[i], "--kernel")) {
       std::string k = next("--kernel");
-      kernel = k == "pixel" ? RM_KERNEL_PIXEL : k == "wavequeue" ? RM_KERNEL_WAVEQUEUE : RM_KERNEL_AUTO;
+      kernel = k == "pixel" ? RM_KERNEL_PIXEL : RM_KERNEL_AUTO;
     } else {
       std::fprintf(stderr, "unknown flag %s\n", argv[i]);
       return 2;

@@ -135,14 +135,14 @@ def test_kernel_timing(rm, gpu):
         assert n == 0
 
 
-@pytest.mark.parametrize("kernel", ["pixel", "wavequeue"])
+@pytest.mark.parametrize("aa", [True, False], ids=["k_sample", "k_pixel"])
 @pytest.mark.parametrize("N,R", [(2, 8), (3, 4), (8, 8)])
 @pytest.mark.parametrize("W", [80, 83])  # 16-B row copies / per-pixel copies in k_unshard
-def test_shards_assemble_to_the_full_frame(rm, gpu, kernel, N, R, W):
+def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, W):
     import torch
     H = 61
-    k = rm.RM_KERNEL_PIXEL if kernel == "pixel" else rm.RM_KERNEL_WAVEQUEUE
-    u = rm.sweep_uniforms(70, 120, 3, True, 0)
+    k = rm.RM_KERNEL_PIXEL
+    u = rm.sweep_uniforms(70, 120, 3, aa, 0)
     full = render(rm, u, W, H, kernel=k)
     cap = rm.shard_rows_cap(H, R, N)
     gathered = torch.zeros((N, cap, W, 4), dtype=torch.uint8, device="cuda")
@@ -169,12 +169,15 @@ def test_full_size_kernels_agree_and_are_deterministic(rm, gpu, cfg):
         a32 = r.read_rgba32f()
         r.dispatch(u)
         a32b = r.read_rgba32f()
-    with rm.Renderer(W, H, outputs=3, kernel=rm.RM_KERNEL_WAVEQUEUE) as r:
+    # an independent implementation of the same scene: the reference scene as a
+    # runtime table through the generic k_table_* kernels (no scene-specific proofs)
+    with rm.Renderer(W, H, outputs=3) as r:
+        r.set_scene(rm.default_scene())
         r.dispatch(u)
         w32 = r.read_rgba32f()
         w8 = r.read_rgba8()
     np.testing.assert_array_equal(a32, a32b)          # idempotent dispatch
-    np.testing.assert_array_equal(a32, w32)           # schedule-independent
+    np.testing.assert_array_equal(a32, w32)           # built-in == table kernel
     np.testing.assert_array_equal(w8, rm.quantize_rgba8(w32))
     assert np.isfinite(a32).all() and (a32[..., 3] == 1.0).all()
 
@@ -183,8 +186,10 @@ def test_full_size_counters_match_between_kernels(rm, gpu):
     W, H = 3840, 2160
     u = rm.sweep_uniforms(44, 120, 3, True, 0)
     cs = []
-    for k in (rm.RM_KERNEL_PIXEL, rm.RM_KERNEL_WAVEQUEUE):
-        with rm.Renderer(W, H, kernel=k, counters=True) as r:
+    for table in (False, True):  # built-in scene kernel / the same scene as a table
+        with rm.Renderer(W, H, counters=True) as r:
+            if table:
+                r.set_scene(rm.default_scene())
             r.dispatch(u)
             cs.append((r.counters(), r.sdf_counts()))
     assert cs[0][0] == cs[1][0]
@@ -260,3 +265,27 @@ def test_graph_back_to_back_frames_keep_their_constants(rm, gpu):
         for f in range(n):
             r.dispatch(us[f])
             np.testing.assert_array_equal(outs[f].cpu().numpy(), r.read_rgba8(), err_msg=f"frame {f}")
+
+
+def test_unshard_with_offset_pointers(rm, gpu):
+    """rm_unshard_rgba8 takes caller device pointers: 4-byte-offset (not 16-B
+    aligned) shard and frame buffers take the per-pixel copy path."""
+    import torch
+    W, H, N, R = 80, 45, 3, 4
+    u = rm.sweep_uniforms(20, 120, 1, False, 0)
+    full = render(rm, u, W, H)
+    cap = rm.shard_rows_cap(H, R, N)
+    gbuf = torch.zeros(N * cap * W * 4 + 16, dtype=torch.uint8, device="cuda")
+    fbuf = torch.zeros(H * W * 4 + 16, dtype=torch.uint8, device="cuda")
+    g0, f0 = gbuf.data_ptr() + 4, fbuf.data_ptr() + 4
+    rs = [rm.Renderer(W, H, row_block=R, shard=i, nshards=N) for i in range(N)]
+    for i, r in enumerate(rs):
+        r.set_output_rgba8(g0 + i * cap * W * 4)
+        r.dispatch(u)
+        r.synchronize()
+    rs[0].unshard_rgba8(g0, f0)
+    rs[0].synchronize()
+    got = fbuf[4:4 + H * W * 4].cpu().numpy().reshape(H, W, 4)
+    np.testing.assert_array_equal(got, full)
+    for r in rs:
+        r.close()

@@ -17,12 +17,10 @@ def gold():
 
 
 @pytest.mark.parametrize("name", sorted(META))
-@pytest.mark.parametrize("kernel", ["pixel", "wavequeue"])
-def test_gpu_matches_golden(rm, gpu, gold, name, kernel):
+def test_gpu_matches_golden(rm, gpu, gold, name):
     m = META[name]
     u = rm.sweep_uniforms(m["frame"], 120, m["bounces"], m["aa"], m["shadow"])
-    k = rm.RM_KERNEL_PIXEL if kernel == "pixel" else rm.RM_KERNEL_WAVEQUEUE
-    with rm.Renderer(m["W"], m["H"], outputs=3, kernel=k, counters=True) as r:
+    with rm.Renderer(m["W"], m["H"], outputs=3, counters=True) as r:
         r.dispatch(u)
         f = r.read_rgba32f()
         q = r.read_rgba8()

@@ -276,3 +276,41 @@ def test_specialise_toggle_and_graph(rm, gpu):
         r.specialize_scene(True)  # the cached module: no second compile
         r.dispatch(frames[0])
         np.testing.assert_array_equal(r.read_rgba32f(), want["a", 0])
+
+
+def _big_table(rm, n=30):
+    """The reference scene's 5 objects repeated along x (40 units apart), one plane."""
+    import ctypes as C
+    out = []
+    for k in range(8):
+        for p in rm.default_scene():
+            if p.type == rm.PRIM_PLANE and k:
+                continue
+            q = rm.rm_primitive()
+            C.memmove(C.byref(q), C.byref(p), C.sizeof(p))
+            if q.type != rm.PRIM_PLANE:
+                q.center[0] += 40.0 * k
+            out.append(q)
+    return out[:n]
+
+
+def test_specialisation_register_bound(rm, gpu):
+    """rm_jit.hip compiles a table for the most waves per SIMD (8, 7, 6) at which
+    its production kernels need no scratch (one fixed 8-wave bound
+    spilled for the reference scene and spilled hundreds of VGPRs for large
+    tables).  The reference scene specialises; a 30-entry table fits no such
+    bound and renders with the generic kernel, with the same image."""
+    u = rm.sweep_uniforms(60, 120, 3, True, 0)
+    with rm.Renderer(96, 64, outputs=OUT) as r:
+        assert r.scene_kernel_waves() == 0  # built-in scene
+        r.specialize_scene(True)
+        r.set_scene(rm.default_scene())
+        assert r.scene_kernel_waves() in (6, 7, 8)
+        big = _big_table(rm)
+        assert len(big) == 30
+        r.set_scene(big)
+        assert r.scene_kernel_waves() == 0
+        r.dispatch(u)
+        got = r.read_rgba32f()
+    want = _render(rm, u, 96, 64, scene=big, counters=False)["rgba32f"]
+    np.testing.assert_array_equal(got, want)

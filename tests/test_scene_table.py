@@ -91,14 +91,43 @@ def _code_object(rm, scene, arch=b"gfx950"):
     return rc, buf.raw
 
 
+def _kernel_private_sizes(co):
+    """private_segment_fixed_size (scratch bytes per lane; u32 at offset 4 of the
+    64-byte kernel descriptor `<kernel>.kd`) of every kernel in an AMDGPU ELF."""
+    import struct
+    shoff, = struct.unpack_from("<Q", co, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", co, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", co, shoff + i * shentsize) for i in range(shnum)]
+    out = {}
+    for name_, type_, flags, addr, off, size, link, info, align, entsize in secs:
+        if type_ != 2:  # SHT_SYMTAB
+            continue
+        stroff = secs[link][4]
+        for k in range(size // 24):
+            st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
+                "<IBBHQQ", co, off + 24 * k)
+            end = co.index(b"\0", stroff + st_name)
+            sym = co[stroff + st_name:end].decode()
+            if sym.endswith(".kd") and st_shndx < shnum:
+                sec = secs[st_shndx]
+                kd = sec[4] + (st_value - sec[3])
+                out[sym[:-3]] = struct.unpack_from("<I", co, kd + 4)[0]
+    return out
+
+
 def test_table_specialises_without_a_device(rm):
     """rm_scene_specialize's hiprtc compile (rm_jit.hip) runs here, without a GPU:
     the embedded rm_table.hip compiles for gfx950 with the table folded in, and
-    the code object holds the four table kernels."""
+    the code object holds the four table kernels.  The register bound is the most
+    waves per SIMD at which the production kernels need no scratch:
+    their kernel descriptors carry a zero private segment."""
     rc, co = _code_object(rm, rm.default_scene())
     assert rc == 0 and co[:4] == b"\x7fELF"
     for name in (b"k_table_pixelILb0E", b"k_table_pixelILb1E", b"k_table_sampleILb0E", b"k_table_sampleILb1E"):
         assert name in co
+    priv = _kernel_private_sizes(co)
+    prod = {k: v for k, v in priv.items() if "ILb0E" in k}
+    assert len(prod) == 2 and all(v == 0 for v in prod.values()), priv
     moved = rm.default_scene()
     moved[0].center[0] = 14.0
     rc2, co2 = _code_object(rm, moved)

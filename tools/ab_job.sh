@@ -15,6 +15,7 @@ if [ "$2" = "parity" ]; then
   done
 fi
 timeout -k 10 600 python -u tools/ab_kernel.py --cfg $CFG --rounds ${ROUNDS:-3} --frames 20 || exit 1
+[ "${BENCH:-1}" = 0 ] && exit 0
 for r in 1 2 3; do
   for so in opengl-raymarching-in-compute-shader_amd/librm.so tools/variants/librm_*.so; do
     RM_LIBRM=$so timeout -k 10 120 python bench.py --no-cpu-baseline --config $CFG --steps 60 --warmup 5 > /tmp/ab.json 2>/dev/null || exit 1

@@ -13,7 +13,7 @@ fi
 pkg=opengl-raymarching-in-compute-shader_amd
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$src/include $*"
 b=$(mktemp -d)
-for f in rm_api rm_kernels rm_wavequeue rm_table; do
+for f in rm_api rm_kernels rm_table; do
   [ -f "$src/$pkg/csrc/$f.hip" ] || continue
   /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/$f.hip" -o "$b/$f.o" &
 done

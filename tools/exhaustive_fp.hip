@@ -1,5 +1,5 @@
 // exhaustive_fp.hip — exhaustive bit-exactness proofs for the cheap f32
-// sequences used by k_wavequeue.  For every input of the
+// sequences used by the render kernels.  For every input of the
 // stated domain, each candidate is compared bit-for-bit with the compiler's
 // correctly-rounded operation (HIP default -fhip-fp32-correctly-rounded-divide-sqrt).
 //   sqrt candidates: all non-negative finite floats (0x00000000..0x7f7fffff)
@@ -150,7 +150,15 @@ __global__ void k_rcp_cand(unsigned long long* cnt, unsigned* first) {
 }
 
 // x / 3 and x / 5 (bounce weights 1/i, glsl:186-187) by the Markstein sequence
-// of div_small, against the IEEE division, over all finite x.
+// (the candidate librm measured and did not adopt: rm_fastmath.hpp div_small is
+// the IEEE division), against the IEEE division, over all finite x.
+__device__ __forceinline__ float cand_div_small(float x, int i) {
+  const float d = (float)i;
+  const float y = (i == 3) ? (1.0f / 3.0f) : (1.0f / 5.0f);
+  const float q = x * y;
+  const float r = __builtin_fmaf(-q, d, x);
+  return q == 0.0f ? q : __builtin_fmaf(r, y, q);  // keeps -0 / 3 == -0
+}
 __global__ void k_div_small(unsigned long long* cnt, unsigned* first) {
   unsigned long long c[4] = {0, 0, 0, 0};
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < 0x100000000ull;
@@ -160,8 +168,8 @@ __global__ void k_div_small(unsigned long long* cnt, unsigned* first) {
     const float x = __uint_as_float(u);
     volatile float d3 = 3.0f, d5 = 5.0f;
     const int reg = fabsf(x) >= 0x1p-100f ? 0 : 1;
-    if (__float_as_uint(rmd::div_small(x, 3)) != __float_as_uint(x / d3)) { c[reg]++; atomicMin(&first[reg], u & 0x7fffffffu); }
-    if (__float_as_uint(rmd::div_small(x, 5)) != __float_as_uint(x / d5)) { c[2 + reg]++; atomicMin(&first[2 + reg], u & 0x7fffffffu); }
+    if (__float_as_uint(cand_div_small(x, 3)) != __float_as_uint(x / d3)) { c[reg]++; atomicMin(&first[reg], u & 0x7fffffffu); }
+    if (__float_as_uint(cand_div_small(x, 5)) != __float_as_uint(x / d5)) { c[2 + reg]++; atomicMin(&first[2 + reg], u & 0x7fffffffu); }
   }
   for (int k = 0; k < 4; ++k) atomicAdd(&cnt[k], c[k]);
 }

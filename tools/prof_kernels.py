@@ -1,7 +1,7 @@
 """Render the bench's sweep frames with one kernel variant (driver for rocprofv3 --pmc).
 
   python tools/prof_kernels.py KIND CFG STEPS
-KIND: pixel | wavequeue | table | table-spec.  The frames are bench.py's own
+KIND: pixel | table | table-spec.  The frames are bench.py's own
 (bench_frames(STEPS): step k renders sweep frame floor(k * 120 / STEPS)), one
 launch each, so the per-launch PMC means describe the benched workload.
 """
@@ -17,7 +17,7 @@ from bench import CONFIGS, bench_frames  # noqa: E402
 kname = sys.argv[1] if len(sys.argv) > 1 else "pixel"
 cfg = CONFIGS[int(sys.argv[2]) if len(sys.argv) > 2 else 3]
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-k = rm.RM_KERNEL_WAVEQUEUE if kname == "wavequeue" else rm.RM_KERNEL_PIXEL
+k = rm.RM_KERNEL_PIXEL
 with rm.Renderer(cfg["width"], cfg["height"], kernel=k) as r:
     if kname == "table-spec":  # the same, with kernels compiled for the table (hiprtc)
         r.specialize_scene(True)

@@ -3,7 +3,6 @@
 #define RM_WAVE_TIMES 1
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_kernels.hip"
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_api.hip"
-#include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_wavequeue.hip"
 #include <algorithm>
 #include <cstdio>
 #include <vector>
