@@ -222,6 +222,10 @@ def main() -> int:
                          "rm_default_scene: the k_table_* kernels, SURVEY 8(f) row 4); table-spec = "
                          "the same with kernels compiled for the table (rm_scene_specialize, hiprtc, "
                          "before the timed region); the image is the built-in scene's")
+    ap.add_argument("--spinup-ms", type=float, default=200.0,
+                    help="before the warmup steps, render sweep frames (untimed) for this long so "
+                         "the GPU reaches its sustained clocks: with the 5-step warmup alone the "
+                         "first timed frames run ~6%% slower (tools/probe_ramp.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="cpu_baseline renders every k-th row of one frame (0: the whole "
@@ -229,6 +233,12 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = nproc, capped at the CPUs this process may run on")
     args = ap.parse_args()
+
+    # stdout carries exactly the one JSON line: library banners written to fd 1
+    # (gloo's connection notice, RCCL's version block) go to stderr until then
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -315,6 +325,24 @@ def main() -> int:
         torch.cuda.synchronize()
 
     frames_timed = bench_frames(args.steps)
+    # ---- spin-up (untimed): sustained load until the GPU's clocks have ramped ----
+    # (rounds of nfl frames; with N > 1 every rank runs the same rounds, as each
+    # frame's gather is a collective: rank 0's clock decides, over the host group)
+    if args.spinup_ms > 0:
+        s0, k = time.perf_counter(), 0
+        while True:
+            for _ in range(nfl):
+                step(frames_timed[k % args.steps])
+                k += 1
+            torch.cuda.synchronize()
+            more = (time.perf_counter() - s0) * 1e3 < args.spinup_ms
+            if dist_on:
+                flag = torch.tensor([1 if more else 0], dtype=torch.int32)
+                dist.broadcast(flag, src=0)
+                more = bool(flag.item())
+            if not more:
+                break
+        nstep[0] = 0
     # ---- warmup (untimed): the first W frames of the same list ----
     for k in range(args.warmup):
         step(frames_timed[k % args.steps])
@@ -454,6 +482,7 @@ def main() -> int:
             "fps": round(frames / elapsed, 3),
             # host time to issue the K steps (rank 0): well below ms_per_step = GPU-bound
             "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4),
+            "spinup_ms": args.spinup_ms,
             "roofline": {"bound": "valu",
                          "achieved": round(valu_issue, 3) if valu_issue else None,
                          "peak": VALU_LANE_PEAK_T, "unit": "T VALU lane-instructions/s",
@@ -474,6 +503,8 @@ def main() -> int:
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)
     for rj in rs:
         rj.close()

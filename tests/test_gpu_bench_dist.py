@@ -42,8 +42,8 @@ def test_bench_rccl_path_at_world_size_one(args):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
                          cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-4000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout[-2000:]
+    lines = out.stdout.strip().splitlines()  # stdout is the JSON line alone (banners: stderr)
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and "RCCL gather" in d["config"]["parallelism"]
     p = d["parity"]

@@ -2,6 +2,8 @@
 # Build a librm variant with extra -D flags for A/B timing (tools/probe_variants.sh).
 #   tools/build_variant.sh NAME [-DFOO=1 ...]   -> tools/variants/librm_NAME.so
 #   tools/build_variant.sh NAME --rev GITREV    -> librm built from a committed revision
+#   tools/build_variant.sh NAME --patch F.diff  -> librm built with a patch applied
+#                                                 (experiments live as patches, not knobs)
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -9,6 +11,11 @@ out=$root/tools/variants; mkdir -p "$out"
 src=$root
 if [ "$1" = "--rev" ]; then
   src=$(mktemp -d); git -C "$root" archive "$2" | tar -x -C "$src"; shift 2
+fi
+if [ "$1" = "--patch" ]; then
+  p=$(cd "$(dirname "$2")" && pwd)/$(basename "$2")
+  if [ "$src" = "$root" ]; then src=$(mktemp -d); (cd "$root" && tar -c --exclude=.git --exclude=gpurun_out --exclude=tools/variants .) | tar -x -C "$src"; fi
+  (cd "$src" && patch -s -p1 < "$p"); shift 2
 fi
 pkg=opengl-raymarching-in-compute-shader_amd
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$src/include $*"
