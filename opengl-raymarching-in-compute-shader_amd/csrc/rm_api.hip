@@ -140,7 +140,7 @@ int nccl_fail(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
 // the values reached here, rm_fastmath.hpp).  The bounds (slack, LB_k, b1, b2)
 // only need to be valid: their 2^-12 / 2^-18 margins were made for v_sqrt's
 // 1.5 ulp, and the IEEE sqrt is within them.
-void prep_host(const float cam[3], float blend, float omblend, float out[12]) {
+void prep_host(const float cam[3], float blend, float omblend, float out[16]) {
   using namespace rmd;
   const float px = cam[0], py = cam[1], pz = cam[2];
   const float ax = px - 15.0f, ay = py, az = pz + 10.0f, bx = px + 25.0f, cx = px + 5.0f;
@@ -175,14 +175,21 @@ void prep_host(const float cam[3], float blend, float omblend, float out[12]) {
   const float kx = px - CAP_MX, ky = py - CAP_MY, kz = pz - CAP_MZ;
   const float x[5] = {x0, x1, xs, (cx2 + ay2) + tz * tz, (kx * kx + ky * ky) + kz * kz};
   const float R[5] = {3.0f, 3.0f, R_BLEND_LO, R_TORUS, R_CAPSULE};
-  std::memset(out, 0, 12 * sizeof(float));
+  std::memset(out, 0, 16 * sizeof(float));
   out[PREP_VALID] = (!nan && d > 0.0f && d <= 400.0f) ? 1.0f : 0.0f;
   out[PREP_D0] = d;
   out[PREP_SLACK] = sl;
-  out[PREP_PL] = (py + 5.5f) + sl;
   out[PREP_B1] = (rc + SH_RALL + sl + 0.0f) * HI;
   out[PREP_B2] = ((py + 5.5f) - sl - 0.0f * HI) - 0x1p-19f * (std::fabs(py) + 5.5f + 0.0f + sl);
-  for (int k = 0; k < 5; ++k) out[PREP_LB + k] = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+  const float pl = (py + 5.5f) + sl;
+  for (int k = 0; k < 5; ++k) {
+    // the gaps of scene_lazy's re-test at the camera with U = d0, in its float
+    // operations: g = (lb - d0) - slack, plane gap lb - pl
+    const float lb = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+    const float g = lb - d - sl;
+    out[PREP_G + k] = g > 0.0f ? g : -INFINITY;
+    out[PREP_H + k] = g > 0.0f ? lb - pl : -INFINITY;
+  }
 }
 
 rmd::Frame make_frame(const rm_ctx* c) {

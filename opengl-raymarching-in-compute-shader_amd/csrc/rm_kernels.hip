@@ -77,22 +77,20 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // provable miss (rm_scene.hpp "early exits"): production stops there; the
   // counting build runs on to the reference's step count and poisons the colour
   // with NaN should the ray hit after all (parity tests compare NaN masks)
-  const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+  // (mx = lin_exit_T(MISS_C, ...), formed where it is used: a downward ray has
+  // mx = +inf, so waves of downward rays never form it)
   bool proven_miss = false;
   int i0 = 1;
   // Primary rays: step 0 is at the camera for every pixel; the host evaluated it
-  // once (its distance is exact, its bounds as the block would form them).
-  // Each lane only turns the bounds into expiries with its own |rd|: the
-  // re-test of scene_lazy with U = d0 (<= the block's running minimum).
+  // once (its distance is exact, its gaps as the block's re-test would form
+  // them with U = d0).  Each lane only turns the gaps into expiries with its own
+  // |rd|: te = max(g / 2|rd|, plane gap / (|rd| + rd.y), 0) at t = 0, where a
+  // gap the host found <= 0 is -inf (te = 0: re-test at the next step).
   if (prep) {
-    const float d0 = F.prepv[PREP_D0], sl = F.prepv[PREP_SLACK], pl = F.prepv[PREP_PL];
+    const float d0 = F.prepv[PREP_D0];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const float lb = F.prepv[PREP_LB + k];
-      const float g = lb - d0 - sl;
-      const float bud = __builtin_fmaxf(g * lc.inv2v, (lb - pl) * lc.invp);
-      lc.te[k] = (g > 0.0f) ? 0.0f + bud : 0.0f;
-    }
+    for (int k = 0; k < 5; ++k)
+      lc.te[k] = vmax3(F.prepv[PREP_G + k] * lc.inv2v, F.prepv[PREP_H + k] * lc.invp, 0.0f);
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
     if (COUNT) c.march++;
     dl = d0;
@@ -119,7 +117,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     // Waves of downward rays only (rd.y <= 0 gives mx = +inf) also drop the mx
     // compare: the hit is their only lane exit.
     const float QNAN = __builtin_nanf("");
-    auto run = [&](auto esc, auto usemx) {
+    auto run = [&](auto esc, auto usemx, const float mx) {
       // The primary march runs in segments ending at kCapI0 and kCapI1: the step
       // loop itself is the plain one, with the segment end as its scalar bound.
       // Between segments a lane's exit test is re-formed from its last (t, dl)
@@ -160,10 +158,17 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
         iend = iend < kCapI1 ? kCapI1 : nmax;  // segments end at I0 < I1 < nmax
       }
     };
-    const bool need_esc = (mx > tmax) && !(rd.y <= 0.0f && ro.y + 5.5f <= tmax);
-    if (__any(need_esc)) run(std::true_type(), std::true_type());
-    else if (!__any(!(mx == __builtin_huge_valf()))) run(std::false_type(), std::false_type());
-    else run(std::false_type(), std::true_type());
+    // rd.y <= 0: lin_exit_T's plane slope a2 = (rd.y - s1 - c) LO - .. is < 0, so
+    // mx = +inf, and with ro.y + 5.5 <= tmax no step escapes (above)
+    const bool down = rd.y <= 0.0f && ro.y + 5.5f <= tmax;
+    if (__all(down)) {
+      run(std::false_type(), std::false_type(), __builtin_huge_valf());
+    } else {
+      const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+      const bool need_esc = (mx > tmax) && !down;
+      if (__any(need_esc)) run(std::true_type(), std::true_type(), mx);
+      else run(std::false_type(), std::true_type(), mx);
+    }
     asm volatile("" : "+v"(t), "+v"(dl));  // re-form the test, not a lane mask kept per step
     if (dl < 0.000001f * t) {
       const f3 q = add(ro, muls(rd, t));
@@ -179,6 +184,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #endif
   // Counting build (and RM_STATS): one exit per step (hit | escape | step cap
   // | proven miss); the proofs are only checked.
+  const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
 #ifdef RM_STATS
   int nst = 0;  // this lane's steps (diagnostic builds)
 #endif

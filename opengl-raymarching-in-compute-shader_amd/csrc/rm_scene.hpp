@@ -93,7 +93,7 @@ struct Frame {
   float* rgba32f;        // [rows][width][4] or null
   uint32_t* sdf_counts;  // [rows][width] or null (counter builds)
   unsigned long long* counters;  // 6 x u64 (counter builds)
-  float prepv[12];       // step 0 of the primary rays (PrepSlot), from the host per frame
+  float prepv[16];       // step 0 of the primary rays (PrepSlot), from the host per frame
   const float* scene;    // runtime scene table (rm_set_scene), TABLE_WORDS per primitive, or null
   int32_t nprims;        // entries in `scene`
   int32_t grid_x, grid_y;  // k_pixel / k_sample grid (rm::pixel_grid): ordinary kernel
@@ -405,11 +405,12 @@ enum PrepSlot : int {
   PREP_VALID = 0,   // 1 when 0 < d0 <= 400 (no hit or escape at step 0)
   PREP_D0 = 1,      // sdf(camera), the step-0 distance (exact, same ops as scene_lazy)
   PREP_SLACK = 2,   // ray_s0(camera): slack(0) of scene_lazy at the camera
-  PREP_PL = 3,      // plane(camera) + slack(0)
-  PREP_LB = 4,      // 5 lower bounds LB_k(camera), as scene_lazy's re-test forms them
-  PREP_B1 = 9,      // lin_exit_b(camera, slack, 0): the miss exit's ro-dependent terms
-  PREP_B2 = 10,
-  PREP_COUNT = 11
+  PREP_G = 3,       // 5 gaps g_k = (LB_k - d0) - slack of the step-0 re-test (LB_k as
+                    // scene_lazy's re-test forms it), or -inf when g_k <= 0 (no budget)
+  PREP_H = 8,       // 5 plane gaps LB_k - (plane(camera) + slack), or -inf when g_k <= 0
+  PREP_B1 = 13,     // lin_exit_b(camera, slack, 0): the miss exit's ro-dependent terms
+  PREP_B2 = 14,
+  PREP_COUNT = 15
 };
 // Per-ray constants shared by the lazy culler and the linear exits: |rd| from
 // one v_sqrt (within 1.5 ulp) and the slack line s0 + s1 t, rounded up with
