@@ -55,17 +55,22 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // (rm_api.hip prep_host: every primary ray starts at the camera)
   const bool prep = !reflected && F.prepv[PREP_VALID] != 0.0f;
   const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
-  float s0, b1, b2;
-  if (prep) {
-    s0 = F.prepv[PREP_SLACK];
-    b1 = F.prepv[PREP_B1];
-    b2 = F.prepv[PREP_B2];
-  } else {
-    s0 = ray_s0(ro);
-    lin_exit_b(ro, s0, 0.0f, b1, b2);
-  }
+  const float s0 = prep ? F.prepv[PREP_SLACK] : ray_s0(ro);
   LazyCull lc;
   lazy_init(lc, rd, rdl, s0, s1);
+  // the provable-miss threshold mx (rm_scene.hpp "early exits"), formed where it
+  // is used: its ro-dependent terms b1, b2 with it (a downward ray has mx = +inf,
+  // so waves of downward rays never form either)
+  auto miss_T = [&]() {
+    float b1, b2;
+    if (prep) {
+      b1 = F.prepv[PREP_B1];
+      b2 = F.prepv[PREP_B2];
+    } else {
+      lin_exit_b(ro, s0, 0.0f, b1, b2);
+    }
+    return lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+  };
   // lin_exit's object bound T1 for the step-cap check, re-formed there from the
   // ray (rare) rather than kept live through the loop
   auto cap_T1 = [&](f3 o, f3 r) {
@@ -74,11 +79,9 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     else lin_exit_b(o, lc.s0, 0.0f, b1c, b2c);
     return lin_exit_T1(MISS_C, ray_rdl(r), lc.s1, b1c);
   };
-  // provable miss (rm_scene.hpp "early exits"): production stops there; the
-  // counting build runs on to the reference's step count and poisons the colour
-  // with NaN should the ray hit after all (parity tests compare NaN masks)
-  // (mx = lin_exit_T(MISS_C, ...), formed where it is used: a downward ray has
-  // mx = +inf, so waves of downward rays never form it)
+  // provable miss: production stops there; the counting build runs on to the
+  // reference's step count and poisons the colour with NaN should the ray hit
+  // after all (parity tests compare NaN masks)
   bool proven_miss = false;
   int i0 = 1;
   // Primary rays: step 0 is at the camera for every pixel; the host evaluated it
@@ -164,7 +167,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     if (__all(down)) {
       run(std::false_type(), std::false_type(), __builtin_huge_valf());
     } else {
-      const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+      const float mx = miss_T();
       const bool need_esc = (mx > tmax) && !down;
       if (__any(need_esc)) run(std::true_type(), std::true_type(), mx);
       else run(std::false_type(), std::true_type(), mx);
@@ -184,7 +187,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #endif
   // Counting build (and RM_STATS): one exit per step (hit | escape | step cap
   // | proven miss); the proofs are only checked.
-  const float mx = lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+  const float mx = miss_T();
 #ifdef RM_STATS
   int nst = 0;  // this lane's steps (diagnostic builds)
 #endif
