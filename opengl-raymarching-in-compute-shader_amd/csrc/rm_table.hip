@@ -337,6 +337,28 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
   const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
   bool proven = false;
   TLazy lz(S, ro, rd);
+  if (!COUNT) {
+    // Production: one exit at the latch (as march<false>, rm_kernels.hip).  The
+    // step at t runs when t <= T and fewer than nmax steps were taken; after it,
+    // the march ends on hit | escape | t + d past T (a NaN t + d fails the
+    // compare; the reference would march on with t = NaN to the cap, also a
+    // miss) | the step cap.  The last step's t is kept, so its hit test re-forms.
+    if (!(0.0f <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+    float tp = 0.0f, d = 0.0f;
+    int k = 0;
+    for (int i = 1;; ++i) {
+      const f3 p = add(ro, muls(rd, t));
+      d = lz.dist(S, p, t, k);
+      tp = t;
+      t = t + d;
+      if ((d < 0.000001f * tp) | (d > tmax) | !(t <= T) | (i >= nmax)) break;
+    }
+    if (d < 0.000001f * tp) {
+      const f3 p = add(ro, muls(rd, tp));
+      return THit{tp, S.id(k), S.material(k), S.color(k, p)};
+    }
+    return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+  }
   for (int i = 0; i < nmax; ++i) {
     if (t > T) {
       if (!COUNT) break;
