@@ -93,6 +93,14 @@ __device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float
       return tlen(sub(pa, muls(ba, h))) - a[7];
     }
     default:  // RM_PRIM_PLANE
+#ifdef RM_TABLE_STATIC
+      // A specialised table's axis-aligned normal (0, n_y, 0), as the reference's
+      // floor (a compile-time test): the x and z terms of the dot are signed
+      // zeros for finite q, which leave the sum as it is (the built-in kernel's
+      // p.y + 5.5, rm_scene.hpp), so q.x and q.z are not read.  (A runtime test
+      // in the generic kernel measured 5 % slower.)
+      if (a[0] == 0.0f && a[2] == 0.0f) return q.y * a[1] + a[3];
+#endif
       return dot(q, mk(a[0], a[1], a[2])) + a[3];
   }
 }
