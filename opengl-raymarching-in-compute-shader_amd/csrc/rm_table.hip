@@ -51,6 +51,9 @@ namespace rmd {
 struct TCnt {
   uint32_t rays, march, reflect, shadow, normals, lights;
 };
+// compile-time flags of the march-loop variants (no <type_traits> under hiprtc)
+struct Yes { static constexpr bool value = true; };
+struct No { static constexpr bool value = false; };
 
 using rm::TABLE_WORDS;
 
@@ -194,6 +197,30 @@ struct Table {
     return mk(P[rm::TW_COLOR], P[rm::TW_COLOR + 1], P[rm::TW_COLOR + 2]);
   }
   __device__ __forceinline__ int id(int k) const { return __float_as_int(entry(k)[rm::TW_ID]); }
+  // True when no step of a march from ro along rd can see a distance > tmax:
+  // some axis-aligned plane (normal (0, n_y, 0), a specialised table's
+  // compile-time test) has a value that does not grow along the ray and starts
+  // at or below tmax.  Its float value RN(RN(q.y n_y) + off), q.y = RN(p.y - c.y),
+  // p.y = RN(ro.y + RN(rd.y t)), is monotone in t (rounding is monotone), non-
+  // increasing when n_y rd.y <= 0, and the minimum is at most that value.  NaNs
+  // fail every compare (false).  The generic kernel proves nothing (false).
+  __device__ __forceinline__ bool no_escape(f3 ro, f3 rd, float tmax) const {
+    bool ok = false;
+#ifdef RM_TABLE_STATIC
+    RM_TS_UNROLL
+    for (int k = 0; k < n; ++k) {
+      const float* P = entry(k);
+      const float* a = P + rm::TW_P;
+      if (type(k) != RM_PRIM_PLANE || !(a[0] == 0.0f && a[2] == 0.0f)) continue;
+      const bool swz = __float_as_int(P[rm::TW_SWIZZLE]) == RM_SWIZZLE_XZY;
+      const float oy = swz ? ro.z : ro.y, ry = swz ? rd.z : rd.y;  // q = (p - c).xzy: q.y = p.z - c.z
+      const float cy = swz ? P[rm::TW_CENTER + 2] : P[rm::TW_CENTER + 1];
+      const bool mono = (a[1] > 0.0f && ry <= 0.0f) || (a[1] < 0.0f && ry >= 0.0f);
+      ok = ok || (mono && (oy - cy) * a[1] + a[3] <= tmax);
+    }
+#endif
+    return ok;
+  }
   __device__ __forceinline__ float material(int k) const { return entry(k)[rm::TW_MATERIAL]; }
 };
 
@@ -354,12 +381,28 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     if (!(0.0f <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
     float tp = 0.0f, d = 0.0f;
     int k = 0;
-    for (int i = 1;; ++i) {
-      const f3 p = add(ro, muls(rd, t));
-      d = lz.dist(S, p, t, k);
-      tp = t;
-      t = t + d;
-      if ((d < 0.000001f * tp) | (d > tmax) | !(t <= T) | (i >= nmax)) break;
+    // Variants of the loop (as march<false>'s): the T compare is dropped when T
+    // is +inf on every lane (a NaN t then marches on to the cap, a miss as
+    // before), the escape test when no lane can escape (S.no_escape).
+    auto run = [&](auto esc, auto useT) {
+      for (int i = 1;; ++i) {
+        const f3 p = add(ro, muls(rd, t));
+        d = lz.dist(S, p, t, k);
+        tp = t;
+        t = t + d;
+        bool ex = (d < 0.000001f * tp) | (i >= nmax);
+        if (decltype(useT)::value) ex = ex | !(t <= T);
+        if (decltype(esc)::value) ex = ex | (d > tmax);
+        if (ex) break;
+      }
+    };
+    const bool useT = __any(!(T == __builtin_huge_valf()));
+    if (__all(S.no_escape(ro, rd, tmax))) {
+      if (useT) run(No(), Yes());
+      else run(No(), No());
+    } else {
+      if (useT) run(Yes(), Yes());
+      else run(Yes(), No());
     }
     if (d < 0.000001f * tp) {
       const f3 p = add(ro, muls(rd, tp));
