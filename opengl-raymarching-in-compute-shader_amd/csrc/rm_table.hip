@@ -166,6 +166,62 @@ struct Table {
     }
     return d;
   }
+  // GetNormal's four samples, sdf at pos and at pos + 0.001 e_x / e_y / e_z
+  // (glsl:278-288), with one culling pass for all four (the generic form of
+  // rm_scene.hpp normal_samples).  The samples lie within e = 0.001 + 2^-22
+  // (|pos|_1 + 1) of pos (the float adds round).  An entry's ball bound is
+  // 1-Lipschitz, so at a sample it is at least its value at pos minus e, and
+  // the minimum there is at most U + L e (U: the planes at pos, L = EX_LIP):
+  // an entry whose bound at pos exceeds U + (1 + L) e (rounded up), with the
+  // slack taken at |pos|_1 + 0.002 >= every sample's |p|_1, is strictly above
+  // the minimum at all four.  The others are evaluated at every sample with
+  // opU in table order, so each value equals dist()'s at that point.  With
+  // have_c0 the centre sample is c0 and is not evaluated.
+  __device__ __forceinline__ void normal_samples(f3 pos, bool have_c0, float& c0, float& vx, float& vy,
+                                                 float& vz) const {
+    const float INF = __builtin_huge_valf();
+    const f3 px = add(pos, mk(0.001f, 0.0f, 0.0f));
+    const f3 py = add(pos, mk(0.0f, 0.001f, 0.0f));
+    const f3 pz = add(pos, mk(0.0f, 0.0f, 0.001f));
+    const float* ex = exits();
+    const float p1 = (fabsf(pos.x) + fabsf(pos.y)) + fabsf(pos.z);
+    float U = INF;
+    RM_TS_UNROLL
+    for (int k = 0; k < n; ++k)
+      if (type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(entry(k), RM_PRIM_PLANE, pos, blend, omblend));
+    const float e = 0.001f + 0x1p-22f * (p1 + 1.0f);
+    const float Ue = U + ((1.0f + ex[rm::EX_LIP]) * e * (1.0f + 0x1p-10f) + 0x1p-20f * fabsf(U));
+    const float slack = ex[rm::EX_SIGMA] * ((p1 + 0.002f) + ex[rm::EX_S]) *
+                        ((1.0f + 0x1p-12f) * (1.0f + 0x1p-12f));
+    uint32_t keep = 0;  // entries not culled at the samples
+    RM_TS_UNROLL
+    for (int k = 0; k < n; ++k) {
+      const float* P = entry(k);
+      bool cull = false;
+      if (P[rm::TW_BALL + 3] != INF && type(k) != RM_PRIM_SPHERE) {
+        const float bx = pos.x - P[rm::TW_BALL], by = pos.y - P[rm::TW_BALL + 1], bz = pos.z - P[rm::TW_BALL + 2];
+        const float x = (bx * bx + by * by) + bz * bz;
+        const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), 1.0f - 0x1p-12f, -(P[rm::TW_BALL + 3] + slack));
+        cull = (lb > Ue) & (x < 0x1p120f);
+      }
+      keep |= cull ? 0u : 1u << k;
+    }
+    // one sample at a time (fewer live values): opU in table order over `keep`
+    auto sample = [&](f3 q) {
+      float d = INF;
+      RM_TS_UNROLL
+      for (int k = 0; k < n; ++k) {
+        if (!((keep >> k) & 1u)) continue;
+        const float v = prim_dist(entry(k), type(k), q, blend, omblend);
+        d = d < v ? d : v;
+      }
+      return d;
+    };
+    if (!have_c0) c0 = sample(pos);
+    vx = sample(px);
+    vy = sample(py);
+    vz = sample(pz);
+  }
   // sdf(p) over the entries whose bit is set in `mask` (the others are proven
   // strictly above the minimum by the march's lazy culling), opU in table order
   // `wave` (uniform) has every bit some lane of the wave has in `mask`.
@@ -359,6 +415,7 @@ struct THit {
   int id;
   float material;
   f3 color;
+  float d;  // a hit's last distance: sdf at the hit point itself (GetNormal's centre sample)
 };
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161
@@ -378,7 +435,7 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     // the march ends on hit | escape | t + d past T (a NaN t + d fails the
     // compare; the reference would march on with t = NaN to the cap, also a
     // miss) | the step cap.  The last step's t is kept, so its hit test re-forms.
-    if (!(0.0f <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+    if (!(0.0f <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
     float tp = 0.0f, d = 0.0f;
     int k = 0;
     // Variants of the loop (as march<false>'s): the T compare is dropped when T
@@ -406,9 +463,9 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     }
     if (d < 0.000001f * tp) {
       const f3 p = add(ro, muls(rd, tp));
-      return THit{tp, S.id(k), S.material(k), S.color(k, p)};
+      return THit{tp, S.id(k), S.material(k), S.color(k, p), d};
     }
-    return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+    return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
   }
   for (int i = 0; i < nmax; ++i) {
     if (t > T) {
@@ -424,22 +481,22 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     }
     if (d < 0.000001f * t)
       return THit{t, S.id(k), S.material(k),
-                  (COUNT && proven) ? mk(__builtin_nanf(""), 0.0f, 0.0f) : S.color(k, p)};
+                  (COUNT && proven) ? mk(__builtin_nanf(""), 0.0f, 0.0f) : S.color(k, p), d};
     if (d > tmax) break;
     t += d;
   }
-  return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f)};
+  return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
 }
 
 // GetNormal glsl:278-288
 template <bool COUNT>
-__device__ RM_TS_INLINE f3 tnormal(const Table& S, f3 pos, TCnt& c) {
+// With have_c0 the centre sample sdf(pos) is c0, the march's last distance at
+// this very point (render's pos == the march's last p, glsl:226 vs :129).
+__device__ RM_TS_INLINE f3 tnormal(const Table& S, f3 pos, TCnt& c, bool have_c0 = false,
+                                   float c0 = 0.0f) {
   if (COUNT) c.normals++;
-  int k;
-  const float c0 = S.dist(pos, k);
-  const float x = S.dist(add(pos, mk(0.001f, 0.0f, 0.0f)), k);
-  const float y = S.dist(add(pos, mk(0.0f, 0.001f, 0.0f)), k);
-  const float z = S.dist(add(pos, mk(0.0f, 0.0f, 0.001f)), k);
+  float x, y, z;
+  S.normal_samples(pos, have_c0, c0, x, y, z);
   return tnormalize(subs(mk(x, y, z), c0));
 }
 
@@ -459,7 +516,7 @@ __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 
     const float h = lz.dist(S, add(ro, muls(rd, t)), t, k);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
-    res = gmin(res, F.k * h / t);
+    res = shadow_min(res, F.k, h, t);  // min(res, k h / t) (rm_scene.hpp: the divide only when it can matter)
     t += h;
   }
   return res;
@@ -504,7 +561,7 @@ __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd,
   const THit h = tmarch<COUNT>(S, ro, rd, false, c);
   if (h.t != -1.0f) {
     const f3 pos = add(ro, muls(rd, h.t));
-    const f3 normal = tnormal<COUNT>(S, pos, c);
+    const f3 normal = tnormal<COUNT>(S, pos, c, true, h.d);
     if (COUNT) c.lights++;
     color = point_light(F, h.color, normal, pos);
     if (h.id == 7) {
