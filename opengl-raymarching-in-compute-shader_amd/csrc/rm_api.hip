@@ -192,6 +192,84 @@ void prep_host(const float cam[3], float blend, float omblend, float out[16]) {
   }
 }
 
+// Step 0 of a table's primary rays (rm_internal.hpp TablePrep), on the host:
+// what the table kernel's first march step computes at the camera, with the
+// device's float operations (rm_table.hip prim_dist: IEEE sqrt and divide,
+// GLSL min/max, opU in table order; x86-64 SSE floats, -ffp-contract=off).
+// The slot bounds only need to be valid: the 2^-12 margin made for v_sqrt
+// covers the IEEE sqrt.  Invalid (TP_VALID = 0) when d0 is not in (0, 400].
+namespace {
+struct H3 {
+  float x, y, z;
+};
+float hgmin(float x, float y) { return y < x ? y : x; }
+float hgmax(float x, float y) { return x < y ? y : x; }
+float hdot(H3 a, H3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+float hlen(H3 a) { return std::sqrt(hdot(a, a)); }
+float hprim(const float* P, H3 p, float blend, float omblend) {
+  int type, swz;
+  std::memcpy(&type, &P[rm::TW_TYPE], 4);
+  std::memcpy(&swz, &P[rm::TW_SWIZZLE], 4);
+  H3 q{p.x - P[rm::TW_CENTER], p.y - P[rm::TW_CENTER + 1], p.z - P[rm::TW_CENTER + 2]};
+  if (swz == RM_SWIZZLE_XZY) q = H3{q.x, q.z, q.y};
+  const float* a = P + rm::TW_P;
+  switch (type) {
+    case RM_PRIM_SPHERE:
+      return hlen(q) - a[0];
+    case RM_PRIM_BOX:
+    case RM_PRIM_BLEND: {
+      const H3 d{std::fabs(q.x) - a[0], std::fabs(q.y) - a[1], std::fabs(q.z) - a[2]};
+      const H3 m{hgmax(d.x, 0.0f), hgmax(d.y, 0.0f), hgmax(d.z, 0.0f)};
+      const float box = hgmin(hgmax(d.x, hgmax(d.y, d.z)), 0.0f) + hlen(m);
+      if (type == RM_PRIM_BOX) return box;
+      return box * omblend + (hlen(q) - a[3]) * blend;
+    }
+    case RM_PRIM_TORUS: {
+      const float l = std::sqrt(q.x * q.x + q.z * q.z) - a[0];
+      return std::sqrt(l * l + q.y * q.y) - a[1];
+    }
+    case RM_PRIM_CAPSULE: {
+      const H3 pa{q.x - a[0], q.y - a[1], q.z - a[2]}, ba{a[3], a[4], a[5]};
+      const float h = hgmin(hgmax(hdot(pa, ba) / a[6], 0.0f), 1.0f);
+      return hlen(H3{pa.x - ba.x * h, pa.y - ba.y * h, pa.z - ba.z * h}) - a[7];
+    }
+    default:
+      return hdot(q, H3{a[0], a[1], a[2]}) + a[3];
+  }
+}
+}  // namespace
+
+void table_prep_host(const uint32_t* words, int32_t n, const float cam[3], float blend, float omblend,
+                     float out[16]) {
+  const float* t = reinterpret_cast<const float*>(words);
+  const float* ex = t + (size_t)n * rm::TABLE_WORDS;
+  const H3 p{cam[0], cam[1], cam[2]};
+  std::memset(out, 0, 16 * sizeof(float));
+  float d = INFINITY, U = INFINITY;
+  for (int32_t k = 0; k < n; ++k) {
+    const float* P = t + (size_t)k * rm::TABLE_WORDS;
+    const float dk = hprim(P, p, blend, omblend);
+    d = d < dk ? d : dk;  // opU(d, dk) = (d < dk) ? d : dk
+    int type;
+    std::memcpy(&type, &P[rm::TW_TYPE], 4);
+    if (type == RM_PRIM_PLANE) U = hgmin(U, dk);
+  }
+  out[rm::TP_VALID] = (d > 0.0f && d <= 400.0f) ? 1.0f : 0.0f;
+  out[rm::TP_D0] = d;
+  // TLazy::dist's step-0 re-test at p = camera (dprev = +inf: U = the planes)
+  const float sig2 = 2.0f * ex[rm::EX_SIGMA];
+  const float a1 = (std::fabs(p.x) + std::fabs(p.y)) + std::fabs(p.z);
+  const float sl0 = (a1 + ex[rm::EX_S]) * (1.0f + 0x1p-16f);
+  const float sl = sig2 * (a1 + sl0) * (1.0f + 0x1p-10f);
+  const int ns = (int)ex[rm::EX_NSLOTS];
+  for (int j = 0; j < ns && j < rm::EX_MAX_SLOTS; ++j) {
+    const float* B = t + (size_t)(int)ex[rm::EX_SLOTS + j] * rm::TABLE_WORDS + rm::TW_BALL;
+    const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
+    const float lb = std::fma(std::sqrt((bx * bx + by * by) + bz * bz), 1.0f - 0x1p-12f, -B[3]);
+    out[rm::TP_G + j] = lb - U - sl;
+  }
+}
+
 rmd::Frame make_frame(const rm_ctx* c) {
   const rm_uniforms& u = c->u;
   rmd::Frame F;
@@ -227,7 +305,8 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.rgba32f = (c->cfg.outputs & RM_OUT_RGBA32F) ? c->d_rgba32f : nullptr;
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
-  prep_host(F.cam_pos, F.blend, F.omblend, F.prepv);
+  if (c->nprims) table_prep_host(c->scene_words.data(), c->nprims, F.cam_pos, F.blend, F.omblend, F.prepv);
+  else prep_host(F.cam_pos, F.blend, F.omblend, F.prepv);
   F.scene = c->nprims ? reinterpret_cast<const float*>(c->d_scene) : nullptr;
   F.nprims = c->nprims;
   rm::pixel_grid(F.width, F.rows, F.aa != 0, &F.grid_x, &F.grid_y);

@@ -52,6 +52,14 @@ enum ExitWord : int {
   EX_END = EX_SLOTS + EX_MAX_SLOTS,
 };
 constexpr int EXIT_WORDS = EX_END;
+// Step 0 of a table's primary rays, formed on the host per frame (rm_api.hip
+// table_prep_host) and passed in Frame::prepv when a table renders: every
+// primary ray starts at the camera, so step 0 is one uniform evaluation.
+enum TablePrep : int {
+  TP_VALID = 0,  // 1 when 0 < d0 <= 400
+  TP_D0 = 1,     // sdf(camera) (opU over the table, the device's float operations)
+  TP_G = 2,      // per lazy slot j (EX_SLOTS): the step-0 re-test's gap (lb - U) - sl
+};
 // Words for n entries plus the exit header.
 constexpr size_t scene_words(int n) { return (size_t)n * TABLE_WORDS + EXIT_WORDS; }
 // Validates prims[0..n) and writes scene_words(n) words to out; returns

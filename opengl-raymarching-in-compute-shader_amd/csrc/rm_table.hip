@@ -420,29 +420,48 @@ struct THit {
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161
 template <bool COUNT>
-__device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c) {
+__device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c,
+                                   const float* prep = nullptr) {
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   float t = 0.0f;
+  int i0 = 0;  // steps already taken
   // provable miss (table_exit_T): production stops there; the counting build
   // runs on and poisons the colour with NaN should the ray hit after all
   const float T = table_exit_T(S.exits(), MISS_C, 0.0f, ro, rd);
   bool proven = false;
   TLazy lz(S, ro, rd);
+  if (prep && prep[rm::TP_VALID] != 0.0f) {
+    // Primary rays: step 0 is at the camera for every pixel; the host evaluated
+    // it (table_prep_host: d0 exact, the slots' gaps as TLazy::dist's step-0
+    // re-test forms them with U = the planes at the camera).  Each lane turns
+    // the gaps into expiries with its own rate: te = max(fma(g, inv, 0), 0).
+    const float d0 = prep[rm::TP_D0];
+#pragma unroll
+    for (int j = 0; j < TLazy::KL; ++j)
+      if (j < lz.ns) lz.te[j] = __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f);
+    lz.temin = lz.te[0];
+#pragma unroll
+    for (int j = 1; j < TLazy::KL; ++j) lz.temin = __builtin_fminf(lz.temin, lz.te[j]);
+    lz.dprev = d0;
+    t = d0;
+    i0 = 1;
+    if (COUNT) c.march++;
+  }
   if (!COUNT) {
     // Production: one exit at the latch (as march<false>, rm_kernels.hip).  The
     // step at t runs when t <= T and fewer than nmax steps were taken; after it,
     // the march ends on hit | escape | t + d past T (a NaN t + d fails the
     // compare; the reference would march on with t = NaN to the cap, also a
     // miss) | the step cap.  The last step's t is kept, so its hit test re-forms.
-    if (!(0.0f <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
+    if (!(t <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
     float tp = 0.0f, d = 0.0f;
     int k = 0;
     // Variants of the loop (as march<false>'s): the T compare is dropped when T
     // is +inf on every lane (a NaN t then marches on to the cap, a miss as
     // before), the escape test when no lane can escape (S.no_escape).
     auto run = [&](auto esc, auto useT) {
-      for (int i = 1;; ++i) {
+      for (int i = 1 + i0;; ++i) {
         const f3 p = add(ro, muls(rd, t));
         d = lz.dist(S, p, t, k);
         tp = t;
@@ -467,7 +486,7 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     }
     return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
   }
-  for (int i = 0; i < nmax; ++i) {
+  for (int i = i0; i < nmax; ++i) {
     if (t > T) {
       if (!COUNT) break;
       proven = true;
@@ -558,7 +577,7 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
 template <bool COUNT>
 __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
-  const THit h = tmarch<COUNT>(S, ro, rd, false, c);
+  const THit h = tmarch<COUNT>(S, ro, rd, false, c, F.prepv);
   if (h.t != -1.0f) {
     const f3 pos = add(ro, muls(rd, h.t));
     const f3 normal = tnormal<COUNT>(S, pos, c, true, h.d);
