@@ -57,6 +57,10 @@ struct No { static constexpr bool value = false; };
 
 using rm::TABLE_WORDS;
 
+// Wave vote on the ballot builtin itself (hiprtc's __any widens the predicate
+// to an int and compares it again: two extra VALU per vote).
+__device__ __forceinline__ bool wany(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+
 // Correctly rounded sqrt of a sum of squares (x >= 0, +inf or NaN).  The fast
 // form is sqrt_cr_nonneg (exact on [0, FLT_MAX], rm_fastmath.hpp) with +inf
 // passed through, so it equals the IEEE sqrt on the whole domain.
@@ -204,7 +208,7 @@ struct Table {
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), 1.0f - 0x1p-12f, -(P[rm::TW_BALL + 3] + slack));
         cull = (lb > Ue) & (x < 0x1p120f);
       }
-      if (__any(!cull)) keep |= 1u << k;
+      if (wany(!cull)) keep |= 1u << k;
     }
     // one sample at a time (fewer live values): opU in table order over `keep`
     // (an entry this lane culled is strictly above its minimum at the sample)
@@ -373,6 +377,13 @@ struct TLazy {
     grow = (__builtin_fmaf(lip, rdl, 1.0f) + sig2 * rd1) * (1.0f + 0x1p-10f);
     dprev = INF;
   }
+  // True when some lane's re-test is due at its t (uniform).
+  __device__ __forceinline__ bool due(float t) const { return ns > 0 && wany(!(t < temin)); }
+  // A step when no lane's re-test is due: the `always` entries.
+  __device__ __forceinline__ float fast(const Table& S, f3 p, int& best) {
+    dprev = S.dist_mask(p, always, best);
+    return dprev;
+  }
   // sdf(p(t)) and its opU winner; p = ro + rd t as the caller computed it.
   __device__ __forceinline__ float dist(const Table& S, f3 p, float t, int& best) {
     uint32_t wmask = always;
@@ -380,13 +391,13 @@ struct TLazy {
     // A step with no re-test evaluates the `always` entries under their
     // compile-time masks: no per-entry mask tests (-4.4 % per cfg3 frame; the
     // generic kernel's ctz loop measured 5.5 % slower split this way).
-    if (!(ns > 0 && __any(!(t < temin)))) {
+    if (!(ns > 0 && wany(!(t < temin)))) {
       dprev = S.dist_mask(p, always, best);
       return dprev;
     }
     {
 #else
-    if (ns > 0 && __any(!(t < temin))) {
+    if (ns > 0 && wany(!(t < temin))) {
 #endif
       const float sl = sig2 * (((fabsf(p.x) + fabsf(p.y)) + fabsf(p.z)) + sl0) * (1.0f + 0x1p-10f);
       float U = __builtin_fmaf(dprev, grow, sl);
@@ -400,7 +411,7 @@ struct TLazy {
 #endif
 #pragma unroll
       for (int j = 0; j < KL; ++j) {
-        if (j < ns && __any(!(t < te[j]))) {
+        if (j < ns && wany(!(t < te[j]))) {
           const int k = (int)ex[rm::EX_SLOTS + j];
           const float* B = S.entry(k) + rm::TW_BALL;
           const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
@@ -409,7 +420,7 @@ struct TLazy {
           const float g = lb - U - sl;
           const bool expired = !(t < te[j]);
           te[j] = __builtin_fmaxf(te[j], __builtin_fmaxf(__builtin_fmaf(g, inv, t), t));
-          if (__any(expired && !(g > 0.0f))) wmask |= 1u << k;
+          if (wany(expired && !(g > 0.0f))) wmask |= 1u << k;
         }
       }
       temin = te[0];
@@ -471,19 +482,40 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     // Variants of the loop (as march<false>'s): the T compare is dropped when T
     // is +inf on every lane (a NaN t then marches on to the cap, a miss as
     // before), the escape test when no lane can escape (S.no_escape).
+    // A specialised table's march is written as two loops: a step that may
+    // re-test, then steps while no lane's re-test is due (the lazy state is
+    // loop-invariant there, so the compiler keeps it in place instead of copying
+    // it around the back edges: -7 % per cfg3 frame).  A lane that ends leaves
+    // both.
     auto run = [&](auto esc, auto useT) {
-      for (int i = 1 + i0;; ++i) {
-        const f3 p = add(ro, muls(rd, t));
-        d = lz.dist(S, p, t, k);
+      int i = 1 + i0;
+      bool ex = false;
+      auto latch = [&]() {
         tp = t;
         t = t + d;
-        bool ex = (d < 0.000001f * tp) | (i >= nmax);
+        ex = (d < 0.000001f * tp) | (i >= nmax);
         if (decltype(useT)::value) ex = ex | !(t <= T);
         if (decltype(esc)::value) ex = ex | (d > tmax);
-        if (ex) break;
-      }
+        ++i;
+      };
+#ifdef RM_TABLE_STATIC
+      do {
+        d = lz.dist(S, add(ro, muls(rd, t)), t, k);
+        latch();
+        while (!ex && !lz.due(t)) {
+          d = lz.fast(S, add(ro, muls(rd, t)), k);
+          latch();
+        }
+      } while (!ex);
+#else
+      // (the generic kernel measured 6 % slower with the two loops)
+      do {
+        d = lz.dist(S, add(ro, muls(rd, t)), t, k);
+        latch();
+      } while (!ex);
+#endif
     };
-    const bool useT = __any(!(T == __builtin_huge_valf()));
+    const bool useT = wany(!(T == __builtin_huge_valf()));
     if (__all(S.no_escape(ro, rd, tmax))) {
       if (useT) run(No(), Yes());
       else run(No(), No());
