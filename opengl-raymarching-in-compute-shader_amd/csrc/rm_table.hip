@@ -667,11 +667,12 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 
 // Waves per SIMD the register allocation must allow.  The per-table specialised
 // kernels (RM_TABLE_STATIC) get the bound from rm_jit.hip: the most waves at
-// which the table's code needs no scratch.  The generic kernel (91 VGPRs
-// unbounded, 5 waves) is fastest bounded to 6 waves (80 VGPRs, 8 spills):
-// table 3.87 -> 3.47 ms per frame.
+// which the table's code needs no scratch.  The generic kernel is latency bound
+// and fastest at 7 waves (72 VGPRs, 15 spilled to 52 B/lane of scratch): cfg3
+// table 3.06 -> 2.87 ms per frame against 6 waves (80 VGPRs, 5 spills); 8 waves
+// (36 spills) measured the same as 7.
 #ifndef RM_TABLE_MIN_WAVES
-#define RM_TABLE_MIN_WAVES 6
+#define RM_TABLE_MIN_WAVES 7
 #endif
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.

@@ -1,0 +1,6 @@
+#!/bin/bash
+# Interleaved A/B of the generic scene-table kernel against tools/variants/librm_*.so, cfg3.
+set -e
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/ab_kernel.py --table --cfg 3 --rounds ${ROUNDS:-3} > gpurun_out/abg.log 2>&1
+cat gpurun_out/abg.log
