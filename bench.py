@@ -97,8 +97,10 @@ def pmc_entry(kernel_name: str, workload: str):
             continue
         if d.get("_meta", {}).get("workload") != workload:
             continue
+        # "k_table_sample<false>" also names its slot instances "k_table_sample<false, 5>"
+        stem = kernel_name[:-1] if kernel_name.endswith(">") else kernel_name
         for k, v in d.items():
-            if kernel_name in k and "hbm_bytes_per_launch" in v:
+            if (kernel_name in k or stem + "," in k) and "hbm_bytes_per_launch" in v:
                 return v, os.path.basename(path)
     return None, None
 

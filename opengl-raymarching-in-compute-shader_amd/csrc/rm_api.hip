@@ -22,7 +22,7 @@
 namespace rm {
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
-hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s);
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s);
 }  // namespace rm
@@ -65,7 +65,7 @@ struct rm_ctx {
   int64_t launches = 0;
   bool graph_on = false;
   int graph_aa = -1;  // AA value the graphs were captured for (grid shape depends on it)
-  int graph_table = -1;  // whether the graph holds the table kernel (1) or the built-in one (0)
+  int graph_table = -1;  // the kernel the graph holds: built-in (0), generic table kernel (1 + its slot instance)
   const rm::JitTable* graph_jit = nullptr;  // the specialised table kernels captured, if any
   rm_graph_slot gs;
   // RCCL-gathered frames (rm_comm_init, or one device of a multi-GPU context)
@@ -238,6 +238,18 @@ float hprim(const float* P, H3 p, float blend, float omblend) {
   }
 }
 }  // namespace
+
+// The lazy slots of the context's table (EX_NSLOTS of its compiled words): the
+// generic table kernel's instance (rm_table.hip launch_table).
+static int table_slots(const rm_ctx* c) {
+  const float* ex = reinterpret_cast<const float*>(c->scene_words.data()) + (size_t)c->nprims * rm::TABLE_WORDS;
+  return (int)ex[rm::EX_NSLOTS];
+}
+// Which kernel a frame renders with (the graph's key): 0 built-in, 1 + the
+// generic table kernel's slot instance.
+static int table_key(const rm_ctx* c) {
+  return c->nprims ? 1 + (table_slots(c) <= rm::TABLE_FEW_SLOTS ? 0 : 1) : 0;
+}
 
 void table_prep_host(const uint32_t* words, int32_t n, const float cam[3], float blend, float omblend,
                      float out[16]) {
@@ -724,7 +736,7 @@ int render_launch(rm_ctx* c) {
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   // a runtime scene table renders with the table kernel
   hipError_t e = c->nprims ? (c->jit ? rm::launch_table_jit(c->jit, F, c->cfg.counters != 0, c->stream)
-                                      : rm::launch_table(F, c->cfg.counters != 0, c->stream))
+                                      : rm::launch_table(F, c->cfg.counters != 0, c->stream, table_slots(c)))
                            : rm::launch_pixel(F, c->cfg.counters != 0, c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
@@ -884,7 +896,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   if (e == hipSuccess) {
     e = !F.nprims ? rm::launch_pixel(F, false, cs)
         : c->jit  ? rm::launch_table_jit(c->jit, F, false, cs)
-                  : rm::launch_table(F, false, cs);
+                  : rm::launch_table(F, false, cs, table_slots(c));
     // the render node: the one node the next captured operation would depend on
     hipStreamCaptureStatus st;
     const hipGraphNode_t* deps = nullptr;
@@ -913,7 +925,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   g.send = render_dst(c);
   g.frame = image_rgba8(c);
   c->graph_aa = F.aa;
-  c->graph_table = F.nprims ? 1 : 0;
+  c->graph_table = table_key(c);
   c->graph_jit = F.nprims ? c->jit : nullptr;
   return RM_OK;
 }
@@ -952,7 +964,7 @@ int graph_frame(rm_ctx* c) {
     // rank takes the same branch, so the collective sequence matches)
     return rm_dispatch(c);
   }
-  if ((F.aa != c->graph_aa || (F.nprims ? 1 : 0) != c->graph_table ||
+  if ((F.aa != c->graph_aa || table_key(c) != c->graph_table ||
        (F.nprims ? c->jit : nullptr) != c->graph_jit || c->gs.send != render_dst(c) ||
        c->gs.frame != image_rgba8(c)) &&
       (rc = graph_capture(c, F)) != RM_OK)

@@ -45,6 +45,9 @@ enum TableWord : int {
 // largest plane |n|; every other entry is 1-Lipschitz).
 constexpr int EX_MAX_PLANES = 4;
 constexpr int EX_MAX_SLOTS = 8;
+// The generic table kernel also comes in an instance holding this many slots,
+// taken for tables that track no more (rm_table.hip launch_table).
+constexpr int TABLE_FEW_SLOTS = 5;
 enum ExitWord : int {
   EX_VALID = 0, EX_CX = 1, EX_CY = 2, EX_CZ = 3, EX_R = 4, EX_SIGMA = 5, EX_S = 6,
   EX_NPLANES = 7, EX_PLANES = 8,  // per plane: world normal n' (3), offset: value ~ dot(p, n') + off
