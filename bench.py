@@ -259,7 +259,8 @@ def main() -> int:
     if dist_on:
         # host-side control only (RCCL ids, barriers, the max over ranks of the time):
         # the frame data moves inside librm, over its own RCCL communicators
-        dist.init_process_group("gloo")
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
 
     cfg = CONFIGS[args.config]
     W, H = cfg["width"], cfg["height"]
@@ -321,6 +322,10 @@ def main() -> int:
         render(j, f)
 
     def barrier():
+        # librm's own wait first: on a communicator context it is bounded
+        # (rm_comm_set_timeout) and turns a hung gather into RM_ERR_COMM
+        for rj in rs:
+            rj.synchronize()
         torch.cuda.synchronize()  # the device: every librm stream
         if dist_on:
             dist.barrier()
@@ -372,21 +377,43 @@ def main() -> int:
         launches += n_j
         rj.enable_timing(False)
     kernel_time_basis = "HIP events on the launch stream over the timed region"
-    if nfl > 1:
-        # Overlapping frames stretch each launch's event interval, so the roofline
-        # takes its kernel time from the same frames rendered one at a time on one
-        # context (HIP events, untimed for `value`).
+    if nfl > 1 or (use_graph and dist_on):
+        # Overlapping frames stretch each launch's event interval (and on a
+        # communicator context a graph launch holds the gather and the assembly
+        # too), so the roofline takes its kernel time from the same frames rendered
+        # one at a time on one context through rm_dispatch, whose HIP events
+        # bracket the render kernel alone (untimed for `value`).
         barrier()
         r.enable_timing(True)
         r.kernel_time_ms(reset=True)
         for f in frames_timed:
-            render(0, f)
+            r.dispatch(uniforms(f))
         barrier()
         kernel_ms, launches = r.kernel_time_ms(reset=True)
         r.enable_timing(False)
-        kernel_time_basis = ("HIP events, the timed frames re-rendered one at a time "
-                             "(the timed region overlaps frames)")
+        kernel_time_basis = ("HIP events around the render kernel, the timed frames re-rendered "
+                             "one at a time through rm_dispatch (the timed region overlaps frames)")
     elapsed = t1 - t0
+    phases = None
+    if dist_on:
+        # per-rank split of one untimed eager frame (rm_frame_phases: HIP events around
+        # the render kernel, the ncclGather and rank 0's assembly), so a scaling
+        # shortfall can be attributed to render imbalance or to the gather
+        r.enable_timing(True)
+        r.dispatch(uniforms(frames_timed[-1]))
+        mine = dict(rank=rank, **{k: round(v, 4) for k, v in r.frame_phases().items()})
+        r.enable_timing(False)
+        r.kernel_time_ms(reset=True)
+        allp = [None] * ws
+        dist.all_gather_object(allp, mine)
+        phases = {"per_rank": allp,
+                  "max_render_ms": max(p["render_ms"] for p in allp),
+                  "max_gather_ms": max(p["gather_ms"] for p in allp),
+                  "assemble_ms": allp[0]["assemble_ms"],
+                  "note": "one untimed frame (the last sweep frame) per rank; gather_ms runs from "
+                          "this rank's render end to its gather end, so it includes waiting for "
+                          "the slowest peer's shard"}
+        barrier()
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -502,6 +529,7 @@ def main() -> int:
                                          "kernel second; the kernel skips most of that work by "
                                          "proof, so this is not a utilisation"},
             "work": cnt_total,
+            "phases": phases,
             "cpu_baseline": cpu,
             "parity": parity,
         }
@@ -516,4 +544,10 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    try:
+        sys.exit(main())
+    except rm.RMError as e:
+        # a communicator failure (RM_ERR_COMM: RCCL error, a peer that died or
+        # stalled past the deadline) ends this rank with a diagnosis, non-zero
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(3 if e.code == rm.RM_ERR_COMM else 4)

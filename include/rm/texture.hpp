@@ -26,10 +26,15 @@ class Texture {
   // texture.cpp:10-21: allocate the image (RGBA8 for display + the RGBA32F
   // storage format of the reference texture).  Returns 0 or an RM_ERR_*.
   // ngpus >= 1: the image is rendered by ngpus devices (device, device+1, ...),
-  // one row-block shard each, gathered with RCCL onto the first (RGBA8 only).
+  // one row-block shard each, gathered with RCCL onto the first.
   int GenerateTexture(int outputs = RM_OUT_RGBA8 | RM_OUT_RGBA32F, int kernel = RM_KERNEL_AUTO,
                       int device = -1, int ngpus = 0) {
-    rm_config cfg = {texWidth, texHeight, device, outputs, kernel, 0, 0, 0, 1, ngpus, nullptr};
+    rm_config cfg;
+    rm_config_init(&cfg, texWidth, texHeight);
+    cfg.device = device;
+    cfg.outputs = outputs;
+    cfg.kernel = kernel;
+    cfg.ngpus = ngpus;
     rm_destroy(texOutput);
     texOutput = nullptr;
     return rm_create(&texOutput, &cfg);

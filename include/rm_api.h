@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RM_API_VERSION 2
+#define RM_API_VERSION 3
 
 /* ---- status codes --------------------------------------------------------- */
 #define RM_OK 0
@@ -46,6 +46,10 @@ extern "C" {
 #define RM_ERR_NOMEM (-3)         /* device or host allocation failed */
 #define RM_ERR_NO_DEVICE (-4)     /* no HIP device (librm never falls back to CPU) */
 #define RM_ERR_STATE (-5)         /* call not valid in this state */
+#define RM_ERR_COMM (-6)          /* RCCL error, or a communicator deadline passed (a peer rank
+                                     failed, stalled or never joined): the communicator was
+                                     aborted; the context reports RM_ERR_COMM from then on and
+                                     can only be destroyed (rm_comm_set_timeout) */
 
 /* ---- output image formats (bitmask for rm_config.outputs) ----------------- */
 #define RM_OUT_RGBA8 1   /* display format (what the quad shows, Quad.glsl:21-25) */
@@ -103,6 +107,10 @@ typedef struct rm_counters {
 } rm_counters;
 
 typedef struct rm_config {
+  /* sizeof(rm_config) (API version 3; rm_config_init sets it).  A host built
+   * against an older header passes a smaller struct whose first word is the
+   * width: rm_create refuses it (RM_ERR_INVALID) instead of reading past it. */
+  uint32_t struct_size;
   int32_t width;      /* image width  (SCREEN_WIDTH,  main.cpp:16) */
   int32_t height;     /* image height (SCREEN_HEIGHT, main.cpp:17) */
   int32_t device;     /* HIP device ordinal; -1 = current device */
@@ -121,12 +129,12 @@ typedef struct rm_config {
    * context drive ngpus devices: devices[0..ngpus), or device, device+1, ...
    * when devices is NULL (device -1 = the current device).  Device i renders
    * shard i of the interleaved row blocks (row_block rows per block, 0 = 8);
-   * ncclGather over a single-process communicator (ncclCommInitAll) collects
+   * ncclGather over a single-process communicator (ncclCommInitRankConfig per device in one group) collects
    * the shards on devices[0], which assembles the frame (k_unshard).  The
    * setters, rm_dispatch, rm_synchronize, rm_read_rgba8, rm_set_scene and the
    * graph calls work as on a one-GPU context; the frame lives on devices[0].
-   * RGBA8 output only, no counters, shard/nshards must be 0.  ngpus = 0: one
-   * device, no RCCL (API version 1 behaviour). */
+   * RGBA8 and/or RGBA32F outputs, no counters, shard/nshards must be 0.
+   * ngpus = 0: one device, no RCCL (API version 1 behaviour). */
   int32_t ngpus;
   const int32_t *devices;
 } rm_config;
@@ -134,6 +142,9 @@ typedef struct rm_config {
 typedef struct rm_ctx rm_ctx;
 
 /* ---- lifetime ------------------------------------------------------------- */
+/* Zero-fills *cfg and sets struct_size, width, height, device = -1 (current),
+ * outputs = RM_OUT_RGBA8, nshards = 1: a one-GPU context with the defaults. */
+int rm_config_init(rm_config *cfg, int32_t width, int32_t height);
 int rm_create(rm_ctx **out, const rm_config *cfg);
 void rm_destroy(rm_ctx *ctx);
 const char *rm_last_error(const rm_ctx *ctx);
@@ -165,7 +176,10 @@ int rm_default_uniforms(rm_uniforms *u);
  * stream (== glDispatchCompute, main.cpp:123). */
 int rm_dispatch(rm_ctx *ctx);
 /* Wait for all work queued on the context (== glMemoryBarrier + the
- * implicit sync of the draw, main.cpp:125-134). */
+ * implicit sync of the draw, main.cpp:125-134).  On a context with a
+ * communicator this wait (and the one inside every readback) is a bounded
+ * poll of the stream and of the communicator's asynchronous error: an RCCL
+ * error or the deadline aborts the communicator and returns RM_ERR_COMM. */
 int rm_synchronize(rm_ctx *ctx);
 /* Synchronous readback. Row 0 of the image is the bottom row (py = 0,
  * quad.hpp:9); flip_y != 0 writes the top row first (image-file order).
@@ -274,6 +288,12 @@ int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
  * launch count since the last reset (synchronizes). */
 int rm_enable_timing(rm_ctx *ctx, int enable);
 int rm_kernel_time_ms(rm_ctx *ctx, double *total_ms, int64_t *launches, int reset);
+/* Phases of the last rm_dispatch issued with timing enabled (synchronizes):
+ * the render kernel, then on a communicator context the gather (render end to
+ * gather end on this rank's stream, so it includes waiting for the slowest
+ * peer's shard) and rank 0's assembly (0 elsewhere).  A multi-GPU context
+ * reports device 0.  RM_ERR_STATE before such a dispatch. */
+int rm_frame_phases(rm_ctx *ctx, double *render_ms, double *gather_ms, double *assemble_ms);
 
 /* ---- one rank per process: RCCL-gathered frames -------------
  * The multi-process form of rm_config.ngpus, for hosts that run one process
@@ -284,14 +304,30 @@ int rm_kernel_time_ms(rm_ctx *ctx, double *total_ms, int64_t *launches, int rese
  * rm_dispatch renders this rank's shard, gathers all shards on rank 0
  * (ncclGather into rank 0's [nranks][rows_cap][width] buffer; rank 0 renders
  * its own shard in place) and, on rank 0, assembles the frame (k_unshard), all
- * on the context's stream.  Rank 0's rm_read_rgba8 / rm_get_output_rgba8 /
- * rm_set_output_rgba8 then refer to the full height x width frame, the other
- * ranks' to their packed shard.  rm_dispatch and rm_graph_dispatch are
- * collective: every rank issues the same sequence.  rm_graph_dispatch captures
- * render + gather + assembly into one hipGraph per rank (cfg 5).  RGBA8 only. */
+ * on the context's stream.  Rank 0's rm_read_rgba8 / rm_read_rgba32f /
+ * rm_get_output_rgba8 / rm_set_output_rgba8 then refer to the full height x
+ * width frame, the other ranks' to their packed shard; an output buffer set on
+ * rank 0 before rm_comm_init (shard-sized) is dropped, so set or re-query output
+ * pointers after it.  rm_dispatch and rm_graph_dispatch are collective: every
+ * rank issues the same sequence.  rm_graph_dispatch captures render + gather +
+ * assembly into one hipGraph per rank (cfg 5).  RGBA8 and/or RGBA32F (16 B/px
+ * shards gathered as ncclFloat32), no counters.
+ *
+ * Failure detection: communicators are non-blocking; rm_comm_init, and every
+ * wait on the context afterwards, polls progress and ncclCommGetAsyncError
+ * against a deadline (rm_comm_set_timeout; default 120000 ms or the
+ * RM_COMM_TIMEOUT_MS environment variable; 0 = none).  A rank that never
+ * joins, an RCCL error or a frame that misses the deadline aborts the
+ * communicator (ncclCommAbort) and returns RM_ERR_COMM with the reason in
+ * rm_last_error; the process and its other contexts stay usable. */
 #define RM_COMM_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
 int rm_comm_unique_id(void *id, size_t size);
 int rm_comm_init(rm_ctx *ctx, const void *id, int32_t nranks, int32_t rank);
+/* Deadline in ms of rm_comm_init and of every later wait on the context. */
+int rm_comm_set_timeout(rm_ctx *ctx, int32_t timeout_ms);
+/* Non-blocking health check: RM_OK, or RM_ERR_COMM when the communicator has
+ * an asynchronous error (it is then aborted) or was aborted before. */
+int rm_comm_check(rm_ctx *ctx);
 /* The context's communicator: rank / size (0 / 1 without one), and the devices
  * a multi-GPU context drives (*ngpus = 1 for a one-GPU context). */
 int rm_comm_info(const rm_ctx *ctx, int32_t *rank, int32_t *nranks, int32_t *ngpus);

@@ -5,6 +5,7 @@
 // rm_create fails with RM_ERR_NO_DEVICE — librm never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -76,6 +77,14 @@ struct rm_ctx {
   int crank = 0, cranks = 1;
   uint8_t* d_gathered = nullptr;  // rank 0: [cranks][rows][width] RGBA8; its own shard renders into slot 0
   uint8_t* d_frame = nullptr;     // rank 0: the assembled [height][width] frame
+  float* d_gathered32 = nullptr;  // the same two for RGBA32F (16 B/px)
+  float* d_frame32 = nullptr;
+  long comm_timeout_ms = 0;       // deadline of every wait on the communicator (0: none)
+  bool comm_failed = false;       // the communicator was aborted (RM_ERR_COMM from then on)
+  std::string comm_why;           // why it was aborted
+  // phase events of the last timed eager dispatch: render start / end, gather end, assembly end
+  hipEvent_t ph[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ph_recorded = false, ph_comm = false;
   // a multi-GPU context (rm_config.ngpus): one shard context per device, subs[0] = rank 0
   std::vector<rm_ctx*> subs;
   std::string err;
@@ -123,6 +132,15 @@ uint8_t* image_rgba8(const rm_ctx* c) {
   if (comm_root(c)) return c->ext_rgba8 ? c->ext_rgba8 : c->d_frame;
   return render_dst(c);
 }
+float* render_dst32(const rm_ctx* c) {
+  if (!(c->cfg.outputs & RM_OUT_RGBA32F)) return nullptr;
+  return comm_root(c) ? c->d_gathered32 : c->d_rgba32f;
+}
+float* image_rgba32f(const rm_ctx* c) {
+  if (!c->subs.empty()) return image_rgba32f(c->subs[0]);
+  if (comm_root(c)) return c->d_frame32;
+  return render_dst32(c);
+}
 int image_rows(const rm_ctx* c) {
   if (!c->subs.empty() || comm_root(c)) return c->cfg.height;
   return c->rows;
@@ -130,7 +148,117 @@ int image_rows(const rm_ctx* c) {
 bool full_frame(const rm_ctx* c) { return c->cfg.nshards <= 1 || !c->subs.empty() || comm_root(c); }
 
 int nccl_fail(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
-  return fail(c, RM_ERR_HIP, std::string(what) + ": " + (r ? r->GetErrorString(e) : "RCCL"));
+  return fail(c, RM_ERR_COMM, std::string(what) + ": " + (r ? r->GetErrorString(e) : "RCCL"));
+}
+
+// ---- communicator failure detection --------------------------------------
+// Every wait on a communicator context is a bounded poll: the stream's progress
+// (hipStreamQuery) and the communicator's asynchronous error
+// (ncclCommGetAsyncError), against c->comm_timeout_ms.  An RCCL error or a missed
+// deadline (a peer that died, stalled or never joined) aborts the communicator
+// (ncclCommAbort: the pending collectives quit) and the context reports
+// RM_ERR_COMM from then on; it can still be read for its error and destroyed.
+long default_comm_timeout_ms() {
+  const char* s = std::getenv("RM_COMM_TIMEOUT_MS");
+  if (s && *s) {
+    char* end = nullptr;
+    const long v = std::strtol(s, &end, 10);
+    if (end && *end == '\0' && v >= 0) return v;
+  }
+  return 120000;
+}
+
+// The contexts whose communicators one frame uses: a multi-GPU context's devices,
+// or the context itself.
+std::vector<rm_ctx*> comm_members(rm_ctx* c) {
+  if (!c->subs.empty()) return c->subs;
+  return {c};
+}
+
+int comm_abort(rm_ctx* c, const std::string& why) {
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  for (rm_ctx* m : comm_members(c)) {
+    if (m->comm && r) {
+      (void)hipSetDevice(m->device);
+      (void)r->CommAbort(m->comm);  // pending collectives see the abort flag and quit
+    }
+    m->comm = nullptr;
+    m->comm_failed = true;
+    m->comm_why = why;
+  }
+  c->comm_failed = true;
+  c->comm_why = why;
+  return fail(c, RM_ERR_COMM, why);
+}
+
+bool has_comm(const rm_ctx* c) { return c->comm || (!c->subs.empty() && c->subs[0]->comm); }
+
+// A communicator context whose communicator was aborted.
+int comm_dead(rm_ctx* c) {
+  return fail(c, RM_ERR_COMM, "the communicator was aborted: " + c->comm_why);
+}
+
+// Waits until every stream of the frame's contexts has drained, polling the
+// communicators' asynchronous errors, within the context's deadline.
+int comm_wait(rm_ctx* c) {
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  const std::vector<rm_ctx*> ms = comm_members(c);
+  const long tmo = c->comm_timeout_ms;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<bool> done(ms.size(), false);
+  for (int spins = 0;; ++spins) {
+    bool all = true;
+    for (size_t i = 0; i < ms.size(); ++i) {
+      if (done[i]) continue;
+      rm_ctx* m = ms[i];
+      (void)hipSetDevice(m->device);
+      const hipError_t q = hipStreamQuery(m->stream);
+      if (q == hipSuccess) {
+        done[i] = true;
+        continue;
+      }
+      if (q != hipErrorNotReady) return hip_fail(c, q, "hipStreamQuery");
+      all = false;
+      if (m->comm) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t e = r->CommGetAsyncError(m->comm, &st);
+        if (e != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+          return comm_abort(c, std::string("RCCL asynchronous error on device ") + std::to_string(m->device) +
+                                   ": " + r->GetErrorString(e != ncclSuccess ? e : st));
+      }
+    }
+    if (all) return RM_OK;
+    if (tmo > 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(tmo))
+      return comm_abort(c, "the frame did not complete within " + std::to_string(tmo) +
+                               " ms (rm_comm_set_timeout): a peer rank stalled, failed or never issued "
+                               "its gather");
+    rm::poll_pause(spins);
+  }
+}
+
+// Waits for an RCCL call that returned ncclInProgress (non-blocking communicator).
+int comm_enqueued(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
+  if (e == ncclSuccess) return RM_OK;
+  if (e != ncclInProgress) return nccl_fail(c, r, e, what);
+  std::vector<ncclComm_t> cs;
+  for (rm_ctx* m : comm_members(c))
+    if (m->comm) cs.push_back(m->comm);
+  const ncclResult_t w = rm::wait_ready(r, cs.data(), (int)cs.size(), c->comm_timeout_ms);
+  if (w == ncclSuccess) return RM_OK;
+  if (w == ncclInProgress)
+    return comm_abort(c, std::string(what) + ": not enqueued within " + std::to_string(c->comm_timeout_ms) + " ms");
+  return comm_abort(c, std::string(what) + ": " + r->GetErrorString(w));
+}
+
+// The stream wait of every synchronising call: bounded on a communicator context.
+int stream_wait(rm_ctx* c) {
+  if (c->comm_failed) return comm_dead(c);
+  if (has_comm(c)) return comm_wait(c);
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  return RM_OK;
 }
 
 // Step 0 of every primary ray (rm_scene.hpp PrepSlot), on the host: what the
@@ -314,7 +442,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.nshards = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
   F.rows = c->rows;
   F.rgba8 = render_dst(c);
-  F.rgba32f = (c->cfg.outputs & RM_OUT_RGBA32F) ? c->d_rgba32f : nullptr;
+  F.rgba32f = render_dst32(c);
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
   if (c->nprims) table_prep_host(c->scene_words.data(), c->nprims, F.cam_pos, F.blend, F.omblend, F.prepv);
@@ -344,21 +472,21 @@ void free_all(rm_ctx* c) {
     if (const rm::Rccl* r = rm::rccl(&err)) (void)r->CommDestroy(c->comm);
   }
   c->comm = nullptr;
-  if (c->d_gathered) (void)hipFree(c->d_gathered);
-  if (c->d_frame) (void)hipFree(c->d_frame);
-  c->d_gathered = nullptr;
-  c->d_frame = nullptr;
-  if (c->d_rgba8) (void)hipFree(c->d_rgba8);
-  if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
-  if (c->d_counts) (void)hipFree(c->d_counts);
-  if (c->d_counters) (void)hipFree(c->d_counters);
-  if (c->d_uv) (void)hipFree(c->d_uv);
-  if (c->d_scene) (void)hipFree(c->d_scene);
+  for (void* p : {(void*)c->d_gathered, (void*)c->d_frame, (void*)c->d_gathered32, (void*)c->d_frame32,
+                  (void*)c->d_rgba8, (void*)c->d_rgba32f, (void*)c->d_counts, (void*)c->d_counters,
+                  (void*)c->d_uv, (void*)c->d_scene})
+    if (p) (void)hipFree(p);
+  c->d_gathered = c->d_frame = nullptr;
+  c->d_gathered32 = c->d_frame32 = nullptr;
   for (auto& p : c->ev_pool) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
   }
   c->ev_pool.clear();
+  for (hipEvent_t& e : c->ph) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   c->d_rgba8 = nullptr;
   c->d_rgba32f = nullptr;
@@ -378,8 +506,11 @@ int check_uniforms(rm_ctx* c, const rm_uniforms& u) {
 }
 
 // Joins a sharded context to a communicator as `rank` of `n`: rank 0 gets the
-// gather buffer (its shard renders into slot 0, so ncclGather runs in place) and
-// the assembled frame.
+// gather buffers (its shard renders into slot 0, so ncclGather runs in place) and
+// the assembled frames, one pair per enabled output format.  Rank 0's readable
+// image changes from its shard to the full frame, so a caller-set RGBA8 output
+// (sized for the shard) is dropped: output pointers are set, or re-queried, after
+// rm_comm_init (include/rm_api.h).
 int comm_attach(rm_ctx* c, ncclComm_t comm, int rank, int n, bool own, bool member) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
@@ -388,29 +519,43 @@ int comm_attach(rm_ctx* c, ncclComm_t comm, int rank, int n, bool own, bool memb
   c->group_member = member;
   c->crank = rank;
   c->cranks = n;
+  c->comm_failed = false;
   if (rank == 0) {
-    const size_t shard = (size_t)c->rows * c->cfg.width * 4, frame = (size_t)c->cfg.height * c->cfg.width * 4;
-    RM_HIP(c, hipMalloc(&c->d_gathered, shard * n));
-    RM_HIP(c, hipMalloc(&c->d_frame, frame));
-    RM_HIP(c, hipMemsetAsync(c->d_gathered, 0, shard * n, c->stream));
-    RM_HIP(c, hipMemsetAsync(c->d_frame, 0, frame, c->stream));
+    const size_t px_shard = (size_t)c->rows * c->cfg.width, px_frame = (size_t)c->cfg.height * c->cfg.width;
+    if (c->cfg.outputs & RM_OUT_RGBA8) {
+      RM_HIP(c, hipMalloc(&c->d_gathered, px_shard * 4 * n));
+      RM_HIP(c, hipMalloc(&c->d_frame, px_frame * 4));
+      RM_HIP(c, hipMemsetAsync(c->d_gathered, 0, px_shard * 4 * n, c->stream));
+      RM_HIP(c, hipMemsetAsync(c->d_frame, 0, px_frame * 4, c->stream));
+    }
+    if (c->cfg.outputs & RM_OUT_RGBA32F) {
+      RM_HIP(c, hipMalloc(&c->d_gathered32, px_shard * 16 * n));
+      RM_HIP(c, hipMalloc(&c->d_frame32, px_frame * 16));
+      RM_HIP(c, hipMemsetAsync(c->d_gathered32, 0, px_shard * 16 * n, c->stream));
+      RM_HIP(c, hipMemsetAsync(c->d_frame32, 0, px_frame * 16, c->stream));
+    }
     RM_HIP(c, hipStreamSynchronize(c->stream));
-    if (c->d_rgba8) (void)hipFree(c->d_rgba8);  // rank 0 renders into the gather buffer
+    // rank 0 renders into the gather buffers
+    if (c->d_rgba8) (void)hipFree(c->d_rgba8);
+    if (c->d_rgba32f) (void)hipFree(c->d_rgba32f);
     c->d_rgba8 = nullptr;
+    c->d_rgba32f = nullptr;
+    c->ext_rgba8 = nullptr;  // a shard-sized caller buffer cannot hold the frame
   }
   graph_release(c);
   return RM_OK;
 }
 
 int check_comm_config(const rm_config& cfg, const char* who) {
-  if ((cfg.outputs & ~RM_OUT_RGBA8) != 0 || cfg.counters)
-    return fail(nullptr, RM_ERR_INVALID, std::string(who) + ": RCCL-gathered frames are RGBA8 only, "
-                                         "without counters");
+  if ((cfg.outputs & ~(RM_OUT_RGBA8 | RM_OUT_RGBA32F)) != 0 || cfg.counters)
+    return fail(nullptr, RM_ERR_INVALID, std::string(who) + ": RCCL-gathered frames are RGBA8 and/or "
+                                         "RGBA32F, without counters");
   return RM_OK;
 }
 
 // rm_config.ngpus >= 1: one shard context per device plus a single-process
-// communicator over the devices (ncclCommInitAll).
+// communicator over the devices (one ncclCommInitRankConfig per device inside a
+// group, non-blocking, waited for within the deadline).
 int create_multi(rm_ctx** out, const rm_config* cfg) {
   const int n = cfg->ngpus;
   int rc = check_comm_config(*cfg, "rm_create");
@@ -434,17 +579,18 @@ int create_multi(rm_ctx** out, const rm_config* cfg) {
   }
   std::string err;
   const rm::Rccl* r = rm::rccl(&err);
-  if (!r) return fail(nullptr, RM_ERR_HIP, "rm_create: " + err);
+  if (!r) return fail(nullptr, RM_ERR_COMM, "rm_create: " + err);
   rm_ctx* c = new (std::nothrow) rm_ctx();
   if (!c) return fail(nullptr, RM_ERR_NOMEM, "rm_create: out of host memory");
   c->cfg = *cfg;
-  c->cfg.outputs = RM_OUT_RGBA8;
+  if (c->cfg.outputs == 0) c->cfg.outputs = RM_OUT_RGBA8;
   c->cfg.row_block = cfg->row_block > 0 ? cfg->row_block : 8;
   c->cfg.nshards = n;
   c->cfg.shard = 0;
   c->cfg.devices = nullptr;  // not kept: the caller owns the array
   c->device = devs[0];
   c->rows = c->cfg.height;
+  c->comm_timeout_ms = default_comm_timeout_ms();
   rm_default_uniforms(&c->u);
   auto bail = [&](int code) {
     g_create_error = c->err;
@@ -464,41 +610,77 @@ int create_multi(rm_ctx** out, const rm_config* cfg) {
     }
     c->subs.push_back(sub);
   }
+  ncclUniqueId id;
+  ncclResult_t e = r->GetUniqueId(&id);
+  if (e != ncclSuccess) return bail(nccl_fail(c, r, e, "ncclGetUniqueId"));
   std::vector<ncclComm_t> comms(n, nullptr);
-  ncclResult_t e = r->CommInitAll(comms.data(), n, devs.data());
-  if (e != ncclSuccess) return bail(nccl_fail(c, r, e, "ncclCommInitAll"));
+  e = r->GroupStart();
+  for (int i = 0; i < n && (e == ncclSuccess || e == ncclInProgress); ++i) {
+    ncclConfig_t nb = rm::nonblocking_config();
+    (void)hipSetDevice(devs[i]);
+    e = r->CommInitRankConfig(&comms[i], n, id, i, &nb);
+  }
+  const ncclResult_t eg = r->GroupEnd();
+  if (e == ncclSuccess || e == ncclInProgress) e = eg;
+  if (e == ncclSuccess || e == ncclInProgress) e = rm::wait_ready(r, comms.data(), n, c->comm_timeout_ms);
+  if (e != ncclSuccess) {
+    for (int i = 0; i < n; ++i)
+      if (comms[i]) (void)r->CommAbort(comms[i]);
+    c->err = e == ncclInProgress
+                 ? "rm_create: the communicator was not ready within " + std::to_string(c->comm_timeout_ms) + " ms"
+                 : std::string("rm_create: ncclCommInitRankConfig: ") + r->GetErrorString(e);
+    return bail(RM_ERR_COMM);
+  }
   for (int i = 0; i < n; ++i) {
     if ((rc = comm_attach(c->subs[i], comms[i], i, n, true, true)) != RM_OK) {
       c->err = c->subs[i]->err;
       for (int j = i + 1; j < n; ++j) (void)r->CommDestroy(comms[j]);
       return bail(rc);
     }
+    c->subs[i]->comm_timeout_ms = c->comm_timeout_ms;
   }
   c->stream = c->subs[0]->stream;  // the frame's stream (not owned)
   *out = c;
   return RM_OK;
 }
 
-// The gather of one rank (ncclGather to rank 0, in place on rank 0).
+// The gather of one rank (ncclGather to rank 0, in place on rank 0): the RGBA8
+// and RGBA32F shards in one group.
 int comm_gather(rm_ctx* c) {
   std::string err;
   const rm::Rccl* r = rm::rccl(&err);
-  if (!r) return fail(c, RM_ERR_HIP, err);
-  const size_t count = (size_t)c->rows * c->cfg.width * 4;
-  const void* send = render_dst(c);
-  void* recv = comm_root(c) ? c->d_gathered : nullptr;
-  const ncclResult_t e = r->Gather(send, recv, count, ncclUint8, 0, c->comm, c->stream);
-  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGather");
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  const size_t px = (size_t)c->rows * c->cfg.width;
+  const bool root = comm_root(c);
+  ncclResult_t e = r->GroupStart();
+  if (e == ncclSuccess && (c->cfg.outputs & RM_OUT_RGBA8))
+    e = r->Gather(render_dst(c), root ? c->d_gathered : nullptr, px * 4, ncclUint8, 0, c->comm, c->stream);
+  if ((e == ncclSuccess || e == ncclInProgress) && (c->cfg.outputs & RM_OUT_RGBA32F))
+    e = r->Gather(render_dst32(c), root ? c->d_gathered32 : nullptr, px * 4, ncclFloat32, 0, c->comm,
+                  c->stream);
+  const ncclResult_t eg = r->GroupEnd();
+  if (e == ncclSuccess || e == ncclInProgress) e = eg;
+  const int rc = comm_enqueued(c, r, e, "ncclGather");
+  if (rc != RM_OK) return rc;
   c->comm_warm = true;
   return RM_OK;
 }
 
-// Rank 0: the gathered shards -> the frame (k_unshard), on the same stream.
+// Rank 0: the gathered shards -> the frame (k_unshard), on the same stream.  An
+// RGBA32F row is 4 x width 32-bit words: the same row permutation as an RGBA8
+// image 4 x as wide.
 int comm_assemble(rm_ctx* c) {
   if (!comm_root(c)) return RM_OK;
-  const hipError_t e = rm::launch_unshard(c->d_gathered, image_rgba8(c), c->cfg.width, c->cfg.height,
-                                          c->cfg.row_block, c->cranks, c->rows, c->stream);
-  if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
+  if (c->cfg.outputs & RM_OUT_RGBA8) {
+    const hipError_t e = rm::launch_unshard(c->d_gathered, image_rgba8(c), c->cfg.width, c->cfg.height,
+                                            c->cfg.row_block, c->cranks, c->rows, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
+  }
+  if (c->cfg.outputs & RM_OUT_RGBA32F) {
+    const hipError_t e = rm::launch_unshard(c->d_gathered32, c->d_frame32, c->cfg.width * 4, c->cfg.height,
+                                            c->cfg.row_block, c->cranks, c->rows, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "unshard launch (RGBA32F)");
+  }
   return RM_OK;
 }
 
@@ -533,9 +715,28 @@ int rm_device_count(int* count) {
   return RM_OK;
 }
 
+int rm_config_init(rm_config* cfg, int32_t width, int32_t height) {
+  if (!cfg) return RM_ERR_INVALID;
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->struct_size = (uint32_t)sizeof(rm_config);
+  cfg->width = width;
+  cfg->height = height;
+  cfg->device = -1;
+  cfg->outputs = RM_OUT_RGBA8;
+  cfg->nshards = 1;
+  return RM_OK;
+}
+
 int rm_create(rm_ctx** out, const rm_config* cfg) {
   if (!out || !cfg) return fail(nullptr, RM_ERR_INVALID, "rm_create: null argument");
   *out = nullptr;
+  // A host built against an older rm_api.h passes a smaller struct without this
+  // field (its first word is the width): refuse it rather than read past its end.
+  if (cfg->struct_size != (uint32_t)sizeof(rm_config))
+    return fail(nullptr, RM_ERR_INVALID,
+                "rm_create: rm_config.struct_size must be sizeof(rm_config) = " +
+                    std::to_string(sizeof(rm_config)) + " (rm_config_init; API version " +
+                    std::to_string(RM_API_VERSION) + ")");
   if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65536 || cfg->height > 65536)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: width/height must be in 1..65536");
   if (cfg->ngpus < 0 || cfg->ngpus > 64)
@@ -627,6 +828,7 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   }
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return bail(hip_fail(c, e, "hipStreamSynchronize"));
   rm_default_uniforms(&c->u);
+  c->comm_timeout_ms = default_comm_timeout_ms();
   *out = c;
   return RM_OK;
 }
@@ -634,6 +836,9 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
 void rm_destroy(rm_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  // a collective that never completes must not hang the teardown: the bounded
+  // wait aborts the communicator on its deadline, and the aborted gather quits
+  if (has_comm(ctx) && !ctx->comm_failed && !ctx->group_member) (void)comm_wait(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   free_all(ctx);
   delete ctx;
@@ -746,29 +951,47 @@ int render_launch(rm_ctx* c) {
 
 int graph_frame(rm_ctx* c);
 
+// Phase k of the frame (0 render start, 1 render end, 2 gather end, 3 assembly
+// end) on the context's stream, when timing is on (rm_frame_phases).
+int phase(rm_ctx* c, int k) {
+  if (!c->timing) return RM_OK;
+  if (!c->ph[k]) RM_HIP(c, hipEventCreate(&c->ph[k]));
+  RM_HIP(c, hipEventRecord(c->ph[k], c->stream));
+  return RM_OK;
+}
+
 // A multi-GPU context's frame: every device renders its shard (plainly or from
 // its render-only graph), one grouped ncclGather collects the shards on device
 // 0 (a single-process communicator needs the group), device 0 assembles.
 int multi_frame(rm_ctx* c, bool graph) {
+  if (c->comm_failed) return comm_dead(c);
   std::string err;
   const rm::Rccl* r = rm::rccl(&err);
-  if (!r) return fail(c, RM_ERR_HIP, err);
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  const bool timed = !graph && c->subs[0]->timing;
+  int rc = RM_OK;
   for (rm_ctx* s : c->subs) {
     s->u = c->u;
-    const int rc = graph ? graph_frame(s) : render_launch(s);
+    if (timed && (rc = phase(s, 0)) != RM_OK) return fail(c, rc, s->err);
+    rc = graph ? graph_frame(s) : render_launch(s);
     if (rc != RM_OK) return fail(c, rc, s->err);
+    if (timed && (rc = phase(s, 1)) != RM_OK) return fail(c, rc, s->err);
   }
   ncclResult_t e = r->GroupStart();
   if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGroupStart");
-  int rc = RM_OK;
   for (rm_ctx* s : c->subs) {
     if ((rc = set_device(s)) != RM_OK || (rc = comm_gather(s)) != RM_OK) break;
   }
   e = r->GroupEnd();
   if (rc != RM_OK) return fail(c, rc, c->subs.empty() ? "" : c->subs[0]->err);
-  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGroupEnd");
-  if ((rc = set_device(c->subs[0])) != RM_OK || (rc = comm_assemble(c->subs[0])) != RM_OK)
-    return fail(c, rc, c->subs[0]->err);
+  if ((rc = comm_enqueued(c, r, e, "ncclGroupEnd (gather)")) != RM_OK) return rc;
+  rm_ctx* s0 = c->subs[0];
+  if ((rc = set_device(s0)) != RM_OK) return fail(c, rc, s0->err);
+  if (timed && (rc = phase(s0, 2)) != RM_OK) return fail(c, rc, s0->err);
+  if ((rc = comm_assemble(s0)) != RM_OK) return fail(c, rc, s0->err);
+  if (timed && (rc = phase(s0, 3)) != RM_OK) return fail(c, rc, s0->err);
+  s0->ph_recorded = timed || s0->ph_recorded;
+  s0->ph_comm = true;
   c->dispatched = true;
   return RM_OK;
 }
@@ -778,27 +1001,33 @@ int multi_frame(rm_ctx* c, bool graph) {
 int rm_dispatch(rm_ctx* c) {
   if (!c) return RM_ERR_INVALID;
   if (!c->subs.empty()) return multi_frame(c, false);
-  int rc = render_launch(c);
-  if (rc != RM_OK) return rc;
+  if (c->comm_failed) return comm_dead(c);
+  int rc;
+  if ((rc = phase(c, 0)) != RM_OK) return rc;
+  if ((rc = render_launch(c)) != RM_OK) return rc;
+  if ((rc = phase(c, 1)) != RM_OK) return rc;
   // one rank of an RCCL-gathered frame: gather on rank 0, which assembles
-  if (c->comm && !c->group_member) {
+  const bool comm = c->comm && !c->group_member;
+  if (comm) {
     if ((rc = comm_gather(c)) != RM_OK) return rc;
+    if ((rc = phase(c, 2)) != RM_OK) return rc;
     if ((rc = comm_assemble(c)) != RM_OK) return rc;
+    if ((rc = phase(c, 3)) != RM_OK) return rc;
+  }
+  if (c->timing) {
+    c->ph_recorded = true;
+    c->ph_comm = comm;
   }
   return RM_OK;
 }
 
 int rm_synchronize(rm_ctx* c) {
   if (!c) return RM_ERR_INVALID;
-  for (rm_ctx* s : c->subs) {
-    const int rc = rm_synchronize(s);
-    if (rc != RM_OK) return fail(c, rc, s->err);
+  if (c->subs.empty()) {
+    const int rc = set_device(c);
+    if (rc != RM_OK) return rc;
   }
-  if (!c->subs.empty()) return RM_OK;
-  int rc = set_device(c);
-  if (rc != RM_OK) return rc;
-  RM_HIP(c, hipStreamSynchronize(c->stream));
-  return RM_OK;
+  return stream_wait(c);
 }
 
 static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t row_pitch,
@@ -818,7 +1047,7 @@ static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t 
   if (row_pitch < w) return fail(c, RM_ERR_INVALID, "row_pitch smaller than a row");
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
-  RM_HIP(c, hipStreamSynchronize(c->stream));
+  if ((rc = stream_wait(c)) != RM_OK) return rc;
   const size_t rows = (size_t)image_rows(c);
   RM_HIP(c, hipMemcpy2D(dst, row_pitch, dev, w, w, rows, hipMemcpyDeviceToHost));
   if (flip_y) {
@@ -844,7 +1073,7 @@ int rm_read_rgba8(rm_ctx* c, uint8_t* dst, size_t row_pitch, int flip_y) {
 
 int rm_read_rgba32f(rm_ctx* c, float* dst, size_t row_pitch, int flip_y) {
   if (!c) return RM_ERR_INVALID;
-  return read_image(c, c->d_rgba32f, 16, dst, row_pitch, flip_y);
+  return read_image(c, image_rgba32f(c), 16, dst, row_pitch, flip_y);
 }
 
 int rm_get_counters(rm_ctx* c, rm_counters* out) {
@@ -954,6 +1183,7 @@ int rm_graph_enable(rm_ctx* c, int enable) {
 
 namespace {
 int graph_frame(rm_ctx* c) {
+  if (c->comm_failed) return comm_dead(c);
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   rmd::Frame F = make_frame(c);
@@ -1193,18 +1423,74 @@ int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
   if (rc != RM_OK) return rc;
   std::string err;
   const rm::Rccl* r = rm::rccl(&err);
-  if (!r) return fail(c, RM_ERR_HIP, "rm_comm_init: " + err);
+  if (!r) return fail(c, RM_ERR_COMM, "rm_comm_init: " + err);
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
   ncclComm_t comm = nullptr;
-  const ncclResult_t e = r->CommInitRank(&comm, nranks, u, rank);
-  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclCommInitRank");
+  // non-blocking init, polled against the deadline: a rank that never joins is
+  // RM_ERR_COMM after comm_timeout_ms, not a host thread blocked forever
+  ncclConfig_t nb = rm::nonblocking_config();
+  ncclResult_t e = r->CommInitRankConfig(&comm, nranks, u, rank, &nb);
+  if ((e == ncclSuccess || e == ncclInProgress) && comm) e = rm::wait_ready(r, &comm, 1, c->comm_timeout_ms);
+  if (e != ncclSuccess) {
+    if (comm) (void)r->CommAbort(comm);
+    if (e == ncclInProgress)
+      return fail(c, RM_ERR_COMM, "rm_comm_init: the communicator was not ready within " +
+                                      std::to_string(c->comm_timeout_ms) +
+                                      " ms (rm_comm_set_timeout): a rank never joined");
+    return nccl_fail(c, r, e, "ncclCommInitRankConfig");
+  }
   RM_HIP(c, hipStreamSynchronize(c->stream));  // frames already queued keep their buffers
   if ((rc = comm_attach(c, comm, rank, nranks, true, false)) != RM_OK) {
     (void)r->CommDestroy(comm);
     c->comm = nullptr;
     return rc;
   }
+  return RM_OK;
+}
+
+int rm_comm_set_timeout(rm_ctx* c, int32_t timeout_ms) {
+  if (!c) return RM_ERR_INVALID;
+  if (timeout_ms < 0) return fail(c, RM_ERR_INVALID, "rm_comm_set_timeout: timeout_ms must be >= 0");
+  c->comm_timeout_ms = timeout_ms;
+  for (rm_ctx* s : c->subs) s->comm_timeout_ms = timeout_ms;
+  return RM_OK;
+}
+
+int rm_comm_check(rm_ctx* c) {
+  if (!c) return RM_ERR_INVALID;
+  if (c->comm_failed) return comm_dead(c);
+  if (!has_comm(c)) return RM_OK;
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  for (rm_ctx* m : comm_members(c)) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t e = r->CommGetAsyncError(m->comm, &st);
+    if (e != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+      return comm_abort(c, std::string("RCCL asynchronous error on device ") + std::to_string(m->device) + ": " +
+                               r->GetErrorString(e != ncclSuccess ? e : st));
+  }
+  return RM_OK;
+}
+
+int rm_frame_phases(rm_ctx* c, double* render_ms, double* gather_ms, double* assemble_ms) {
+  if (!c) return RM_ERR_INVALID;
+  rm_ctx* t = c->subs.empty() ? c : c->subs[0];
+  if (!t->ph_recorded) return fail(c, RM_ERR_STATE, "no timed eager dispatch yet (rm_enable_timing, rm_dispatch)");
+  int rc = set_device(t);
+  if (rc != RM_OK) return rc;
+  if ((rc = stream_wait(c)) != RM_OK) return rc;
+  (void)set_device(t);
+  float ms[3] = {0.0f, 0.0f, 0.0f};
+  RM_HIP(c, hipEventElapsedTime(&ms[0], t->ph[0], t->ph[1]));
+  if (t->ph_comm) {
+    RM_HIP(c, hipEventElapsedTime(&ms[1], t->ph[1], t->ph[2]));
+    RM_HIP(c, hipEventElapsedTime(&ms[2], t->ph[2], t->ph[3]));
+  }
+  if (render_ms) *render_ms = ms[0];
+  if (gather_ms) *gather_ms = ms[1];
+  if (assemble_ms) *assemble_ms = ms[2];
   return RM_OK;
 }
 

@@ -3,7 +3,9 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <type_traits>
 
 namespace rm {
@@ -38,8 +40,10 @@ void load() {
   };
   sym("ncclGetUniqueId", g_rccl.GetUniqueId);
   sym("ncclCommInitRank", g_rccl.CommInitRank);
-  sym("ncclCommInitAll", g_rccl.CommInitAll);
+  sym("ncclCommInitRankConfig", g_rccl.CommInitRankConfig);
   sym("ncclCommDestroy", g_rccl.CommDestroy);
+  sym("ncclCommAbort", g_rccl.CommAbort);
+  sym("ncclCommGetAsyncError", g_rccl.CommGetAsyncError);
   sym("ncclGroupStart", g_rccl.GroupStart);
   sym("ncclGroupEnd", g_rccl.GroupEnd);
   sym("ncclGather", g_rccl.Gather);
@@ -54,6 +58,37 @@ const Rccl* rccl(std::string* err) {
   std::call_once(g_once, load);
   if (!g_ok && err) *err = g_err;
   return g_ok;
+}
+
+ncclConfig_t nonblocking_config() {
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  return cfg;
+}
+
+void poll_pause(int spins) {
+  if (spins < 64) std::this_thread::yield();
+  else std::this_thread::sleep_for(std::chrono::microseconds(spins < 256 ? 50 : 1000));
+}
+
+ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long timeout_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spins = 0;; ++spins) {
+    bool pending = false;
+    for (int i = 0; i < n; ++i) {
+      if (!comms[i]) continue;
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t e = r->CommGetAsyncError(comms[i], &st);
+      if (e != ncclSuccess) return e;
+      if (st == ncclInProgress) pending = true;
+      else if (st != ncclSuccess) return st;
+    }
+    if (!pending) return ncclSuccess;
+    if (timeout_ms > 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+      return ncclInProgress;
+    poll_pause(spins);
+  }
 }
 
 }  // namespace rm

@@ -17,8 +17,10 @@ namespace rm {
 struct Rccl {
   decltype(&ncclGetUniqueId) GetUniqueId;
   decltype(&ncclCommInitRank) CommInitRank;
-  decltype(&ncclCommInitAll) CommInitAll;
+  decltype(&ncclCommInitRankConfig) CommInitRankConfig;
   decltype(&ncclCommDestroy) CommDestroy;
+  decltype(&ncclCommAbort) CommAbort;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError;
   decltype(&ncclGroupStart) GroupStart;
   decltype(&ncclGroupEnd) GroupEnd;
   decltype(&ncclGather) Gather;
@@ -29,5 +31,20 @@ struct Rccl {
 // The loaded entry points, or nullptr with *err set (no RCCL on this host, or one
 // without ncclGather).  Thread-safe; loads once per process.
 const Rccl* rccl(std::string* err);
+
+// Every communicator librm creates is non-blocking (ncclConfig_t.blocking = 0):
+// init and enqueue calls may return ncclInProgress, and their progress is polled
+// with ncclCommGetAsyncError against a deadline, so a peer that never joins or a
+// collective that never completes becomes an error (RM_ERR_COMM) instead of a
+// host thread blocked forever.  SURVEY 5 "Failure detection".
+ncclConfig_t nonblocking_config();
+
+// Polls ncclCommGetAsyncError on comms[0..n) until none is ncclInProgress.
+// Returns ncclSuccess, the first error, or ncclInProgress when timeout_ms (> 0)
+// passed first (timeout_ms <= 0: no deadline).
+ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long timeout_ms);
+
+// Back-off for host polling loops: yields first, then sleeps up to 1 ms.
+void poll_pause(int spins);
 
 }  // namespace rm

@@ -30,6 +30,7 @@ RM_ERR_HIP = -2
 RM_ERR_NOMEM = -3
 RM_ERR_NO_DEVICE = -4
 RM_ERR_STATE = -5
+RM_ERR_COMM = -6
 
 RM_OUT_RGBA8 = 1
 RM_OUT_RGBA32F = 2
@@ -74,7 +75,7 @@ class rm_counters(C.Structure):
 
 
 class rm_config(C.Structure):
-    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
+    _fields_ = [("struct_size", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
                 ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
                 ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32),
                 ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
@@ -144,6 +145,7 @@ _P = C.c_void_p
 _SIGS = {
     "rm_api_version": (C.c_int, []),
     "rm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rm_config_init": (C.c_int, [C.POINTER(rm_config), C.c_int32, C.c_int32]),
     "rm_create": (C.c_int, [C.POINTER(_P), C.POINTER(rm_config)]),
     "rm_destroy": (None, [_P]),
     "rm_last_error": (C.c_char_p, [_P]),
@@ -171,6 +173,8 @@ _SIGS = {
     "rm_unshard_rgba8": (C.c_int, [_P, _P, _P]),
     "rm_enable_timing": (C.c_int, [_P, C.c_int]),
     "rm_kernel_time_ms": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]),
+    "rm_frame_phases": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_double)]),
     "rm_shard_rows_cap": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "rm_shard_global_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rm_camera_init": (C.c_int, [C.POINTER(rm_camera_state), C.c_int32, C.c_int32, C.c_float,
@@ -203,6 +207,8 @@ _SIGS = {
     "rm_comm_init": (C.c_int, [_P, C.c_void_p, C.c_int32, C.c_int32]),
     "rm_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                C.POINTER(C.c_int32)]),
+    "rm_comm_set_timeout": (C.c_int, [_P, C.c_int32]),
+    "rm_comm_check": (C.c_int, [_P]),
 }
 COMM_ID_BYTES = 128
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -381,9 +387,10 @@ class Renderer:
         devs = (C.c_int32 * len(devices))(*devices) if devices else None
         if devices:
             ngpus = len(devices)
-        cfg = rm_config(width=width, height=height, device=device, outputs=outputs,
-                        kernel=kernel, counters=1 if counters else 0, row_block=row_block,
-                        shard=shard, nshards=nshards, ngpus=ngpus,
+        cfg = rm_config(struct_size=C.sizeof(rm_config), width=width, height=height,
+                        device=device, outputs=outputs, kernel=kernel,
+                        counters=1 if counters else 0, row_block=row_block, shard=shard,
+                        nshards=nshards, ngpus=ngpus,
                         devices=C.cast(devs, C.POINTER(C.c_int32)) if devs else None)
         h = C.c_void_p()
         _check(lib().rm_create(C.byref(h), C.byref(cfg)))
@@ -543,6 +550,20 @@ class Renderer:
         _check(lib().rm_comm_init(self._h, buf, nranks, rank), self._h)
         if rank == 0:
             self.rows = self.height
+
+    def comm_set_timeout(self, timeout_ms: int) -> None:
+        """Deadline of rm_comm_init and of every later wait on this context (0: none)."""
+        _check(lib().rm_comm_set_timeout(self._h, int(timeout_ms)), self._h)
+
+    def comm_check(self) -> None:
+        """Non-blocking health check of the communicator (raises RMError RM_ERR_COMM)."""
+        _check(lib().rm_comm_check(self._h), self._h)
+
+    def frame_phases(self) -> dict:
+        """render / gather / assembly ms of the last timed eager dispatch (rm_frame_phases)."""
+        r, g, a = C.c_double(0), C.c_double(0), C.c_double(0)
+        _check(lib().rm_frame_phases(self._h, C.byref(r), C.byref(g), C.byref(a)), self._h)
+        return {"render_ms": r.value, "gather_ms": g.value, "assemble_ms": a.value}
 
     def comm_info(self) -> tuple:
         r, n, g = C.c_int32(0), C.c_int32(0), C.c_int32(0)

@@ -44,7 +44,7 @@ def test_structs_match_header_sizes(rm):
     assert C.sizeof(rm.rm_light) == 60
     assert C.sizeof(rm.rm_uniforms) == 64 + 60 + 4 * 5 + 12 + 8 + 4
     assert C.sizeof(rm.rm_counters) == 56
-    assert C.sizeof(rm.rm_config) == 48  # 10 int32 + the devices pointer
+    assert C.sizeof(rm.rm_config) == 56  # struct_size + 10 int32 (+4 pad) + the devices pointer
     assert C.sizeof(rm.rm_camera_state) == 8 + 24 + 48
 
 
@@ -74,13 +74,28 @@ def test_struct_layouts_match_the_c_compiler(rm, tmp_path):
 
 
 def test_api_version(rm):
-    assert rm.lib().rm_api_version() == 2
+    assert rm.lib().rm_api_version() == 3
+
+
+def test_config_struct_size_is_checked(rm):
+    """a host built against an older rm_api.h passes a smaller
+    rm_config without struct_size (its first word is the width); rm_create
+    refuses it before reading any later field."""
+    cfg = rm.rm_config()
+    assert rm.lib().rm_config_init(C.byref(cfg), 64, 32) == 0
+    assert (cfg.struct_size, cfg.width, cfg.height, cfg.device, cfg.outputs, cfg.nshards,
+            cfg.ngpus) == (C.sizeof(rm.rm_config), 64, 32, -1, rm.RM_OUT_RGBA8, 1, 0)
+    old = rm.rm_config(struct_size=3840, width=2160, height=-1)  # a v1/v2 layout read as v3
+    h = C.c_void_p()
+    assert rm.lib().rm_create(C.byref(h), C.byref(old)) == rm.RM_ERR_INVALID
+    assert b"struct_size" in rm.lib().rm_last_error(None)
+    assert not h.value
 
 
 def test_multi_gpu_config_validation_without_gpu(rm):
-    # RCCL-gathered frames are RGBA8 only, without counters; rejected before any device call
+    # RCCL-gathered frames are RGBA8 / RGBA32F, without counters; rejected before any device call
     with pytest.raises(rm.RMError) as e:
-        rm.Renderer(64, 64, ngpus=2, outputs=rm.RM_OUT_RGBA32F)
+        rm.Renderer(64, 64, ngpus=2, outputs=4)
     assert e.value.code == rm.RM_ERR_INVALID
     with pytest.raises(rm.RMError) as e:
         rm.Renderer(64, 64, ngpus=2, counters=True)

@@ -48,3 +48,20 @@ def test_bench_rccl_path_at_world_size_one(args):
     assert d["n_gpus"] == 1 and "RCCL gather" in d["config"]["parallelism"]
     p = d["parity"]
     assert p["assembled_equals_single_gpu"] and p["max_abs_delta_rgba8"] == 0, p
+    ph = d["phases"]  # per-rank render / gather / assembly split
+    assert len(ph["per_rank"]) == 1 and ph["max_render_ms"] > 0 and ph["assemble_ms"] > 0, ph
+    assert "render kernel" in d["roofline"]["kernel_time_basis"] or args[-1] == "0"
+
+
+@pytest.mark.gpu
+def test_bench_exits_nonzero_on_a_communicator_failure():
+    """A gather that misses the communicator deadline ends bench.py with a
+    diagnosis and a non-zero status (RM_ERR_COMM -> exit 3), never a hang: a
+    1 ms deadline (RM_COMM_TIMEOUT_MS) cannot be met by a 4K frame."""
+    env = dict(os.environ, RM_BENCH_FORCE_DIST="1", RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RM_COMM_TIMEOUT_MS="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3",
+                          "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], env=env,
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 3, (out.returncode, out.stderr[-3000:])
+    assert "librm error -6" in out.stderr and out.stdout.strip() == ""

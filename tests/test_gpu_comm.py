@@ -123,8 +123,8 @@ def test_comm_graph_captures_render_gather_and_assembly(rm, gpu):
 
 def test_comm_init_validation(rm, gpu):
     cid = rm.comm_unique_id()
-    with rm.Renderer(32, 32, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
-        with pytest.raises(rm.RMError) as e:  # RGBA8 only
+    with rm.Renderer(32, 32, counters=True) as r:
+        with pytest.raises(rm.RMError) as e:  # no counters on gathered frames
             r.comm_init(cid, 1, 0)
         assert e.value.code == rm.RM_ERR_INVALID
     with rm.Renderer(32, 32, row_block=8, shard=1, nshards=2) as r:
@@ -151,3 +151,151 @@ def test_frameloop_on_a_multi_gpu_context(rm, gpu, tmp_path):
         assert p.returncode == 0, p.stderr
         outs[name] = ppm.read_bytes()
     assert outs["gpus"] == outs["plain"] and outs["graph"] == outs["plain"]
+
+
+def _reference32(rm, W, H, us):
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
+        out = []
+        for u in us:
+            r.dispatch(u)
+            out.append((r.read_rgba8(), r.read_rgba32f()))
+        return out
+
+
+@pytest.mark.parametrize("form", ["comm_init", "ngpus", "comm_init-graph"])
+def test_gathered_rgba32f_equals_one_gpu_render(rm, gpu, form):
+    """the reference texture's true storage (RGBA32F, texture.cpp:19)
+    on RCCL-gathered frames: 16 B/px shards gathered as ncclFloat32 and assembled by
+    k_unshard (a row of 4 x width words); bit-identical to a one-GPU render."""
+    W, H, R = 160, 90, 8
+    us = _frames(rm, 3)
+    ref = _reference32(rm, W, H, us)
+    outs = rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F
+    if form == "ngpus":
+        r = rm.Renderer(W, H, outputs=outs, ngpus=1, row_block=R)
+    else:
+        r = rm.Renderer(W, H, outputs=outs, row_block=R, shard=0, nshards=1)
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+    with r:
+        if form.endswith("graph"):
+            r.graph_enable(True)
+        for u, (want8, want32) in zip(us, ref):
+            (r.graph_dispatch if form.endswith("graph") else r.dispatch)(u)
+            np.testing.assert_array_equal(r.read_rgba8(), want8)
+            np.testing.assert_array_equal(r.read_rgba32f().view(np.uint32), want32.view(np.uint32))
+    # RGBA32F alone (no RGBA8) gathers too
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA32F, row_block=R, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        r.dispatch(us[0])
+        np.testing.assert_array_equal(r.read_rgba32f().view(np.uint32), ref[0][1].view(np.uint32))
+
+
+def test_output_set_before_comm_init_is_dropped_on_rank0(rm, gpu):
+    """ADVICE r02: a caller RGBA8 buffer set before rm_comm_init is shard-sized;
+    rank 0's image becomes the full frame, so the buffer is dropped (no
+    out-of-bounds assembly into it) and the output pointer is re-queried."""
+    import torch
+    W, H = 96, 64
+    u = _frames(rm, 1)[0]
+    want = _reference(rm, W, H, [u])[0]
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=1) as r:
+        small = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(small.data_ptr())
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        p = r.output_rgba8_ptr()
+        assert p and p != small.data_ptr()
+        r.dispatch(u)
+        np.testing.assert_array_equal(r.read_rgba8(), want)
+        r.synchronize()
+        assert int(small.sum().item()) == 0  # never written
+        big = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(big.data_ptr())  # set after rm_comm_init: the frame's destination
+        r.dispatch(u)
+        r.synchronize()
+        np.testing.assert_array_equal(big.cpu().numpy(), want)
+
+
+def test_comm_init_never_joined_rank_times_out(rm, gpu):
+    """rm_comm_init of rank 0 of 2 whose peer never joins returns
+    RM_ERR_COMM within the deadline (non-blocking init, ncclCommAbort), and the
+    process stays usable: the same context joins a one-rank communicator and
+    renders, and a fresh context renders."""
+    import time
+    W, H = 64, 48
+    u = _frames(rm, 1)[0]
+    want = _reference(rm, W, H, [u])[0]
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=2) as r:
+        r.comm_set_timeout(3000)
+        t0 = time.monotonic()
+        with pytest.raises(rm.RMError) as e:
+            r.comm_init(rm.comm_unique_id(), 2, 0)
+        dt = time.monotonic() - t0
+        assert e.value.code == rm.RM_ERR_COMM, e.value
+        assert "never joined" in str(e.value)
+        assert 2.5 < dt < 30.0, dt
+        assert r.comm_info() == (0, 1, 1)  # no communicator attached
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        r.comm_check()
+        r.dispatch(u)
+        np.testing.assert_array_equal(r.read_rgba8(), want)
+
+
+def test_stalled_frame_hits_the_deadline_and_aborts(rm, gpu):
+    """The bounded wait of rm_synchronize on a communicator context: a stream that
+    does not drain within the deadline (here a spin kernel queued behind the
+    gathered frame stands in for a peer that never sends) aborts the
+    communicator and returns RM_ERR_COMM; later calls report it; the context is
+    destroyed cleanly once the stream drains."""
+    import time
+    import torch
+    W, H = 64, 48
+    u = _frames(rm, 1)[0]
+    want = _reference(rm, W, H, [u])[0]
+    s = torch.cuda.Stream()
+    r = rm.Renderer(W, H, row_block=8, shard=0, nshards=1)
+    r.set_stream(s.cuda_stream)
+    r.comm_init(rm.comm_unique_id(), 1, 0)
+    r.dispatch(u)
+    np.testing.assert_array_equal(r.read_rgba8(), want)
+    r.comm_set_timeout(300)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(int(6e9))  # ~2-3 s of spinning on the context's stream
+    t0 = time.monotonic()
+    with pytest.raises(rm.RMError) as e:
+        r.synchronize()
+    assert e.value.code == rm.RM_ERR_COMM and "did not complete within 300 ms" in str(e.value)
+    # the deadline fires at 300 ms; ncclCommAbort then waits for the device work
+    # already queued to quiesce (here the spin kernel, ~2-3 s), so no hang, no more
+    assert time.monotonic() - t0 < 30.0
+    with pytest.raises(rm.RMError) as e:
+        r.dispatch(u)
+    assert e.value.code == rm.RM_ERR_COMM and "aborted" in str(e.value)
+    with pytest.raises(rm.RMError) as e:
+        r.comm_check()
+    assert e.value.code == rm.RM_ERR_COMM
+    s.synchronize()
+    r.close()
+    with rm.Renderer(W, H) as q:  # the process and the device stay usable
+        q.dispatch(u)
+        np.testing.assert_array_equal(q.read_rgba8(), want)
+
+
+def test_frame_phases_split_render_gather_assembly(rm, gpu):
+    """The per-phase times bench.py's N > 1 line reports (render, gather,
+    assembly), from HIP events on the context's stream."""
+    W, H = 640, 360
+    u = _frames(rm, 1)[0]
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        with pytest.raises(rm.RMError):
+            r.frame_phases()  # no timed dispatch yet
+        r.enable_timing(True)
+        r.dispatch(u)
+        ph = r.frame_phases()
+        assert ph["render_ms"] > 0 and ph["gather_ms"] >= 0 and ph["assemble_ms"] > 0, ph
+    with rm.Renderer(W, H) as r:
+        r.enable_timing(True)
+        r.dispatch(u)
+        ph = r.frame_phases()
+        assert ph["render_ms"] > 0 and ph["gather_ms"] == 0 and ph["assemble_ms"] == 0

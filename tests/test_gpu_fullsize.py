@@ -1,57 +1,98 @@
-"""The production kernels at BASELINE.json's full sizes, against the CPU oracle.
+"""The production kernels on WHOLE frames at every BASELINE.json size, against the CPU oracle.
 
 Reference: shaders/computeShader.glsl:291-344 (one pixel, 1 or 4 samples),
 dispatched per frame by main.cpp:92-147.  The renderers here are created with
 counters off, so they run the kernels bench.py times (k_sample<false> /
 k_pixel<false>, every early exit taken), not the counting build.  The oracle
-renders a row sample of the same frames (all of them would take minutes on the
-host); the bars are the parity bars of tests/test_gpu_parity.py: RGBA8 within
-1 LSB, RGBA32F within 2e-6 with the same NaN mask.
+renders every row of the same frames with all the host threads this process may
+use (the box's 16-CPU share renders a 4K 3-bounce frame in ~2 s).
+
+Bars: RGBA8 within 1 LSB per channel (north_star allows
+2 ULP), RGBA32F within 2e-6 with the same NaN mask.  Each frame's report (per
+channel max |delta|, the |delta| histogram, pixels over 2 LSB) is printed and,
+when RM_PARITY_REPORT names a file, appended to it as one JSON line per frame.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def _rows(H, n, seed):
-    """Fixed rows (bottom, top, the middle band where the horizon and the longest
-    marches are) plus a seeded random sample."""
-    fixed = {0, 1, H // 4, H // 2 - 1, H // 2, H // 2 + 1, H // 2 + H // 20, 3 * H // 4, H - 1}
-    rng = np.random.default_rng(seed)
-    extra = set(int(x) for x in rng.choice(H, size=n, replace=False))
-    return sorted(fixed | extra)
+def _host_threads() -> int:
+    """CPUs this process may use: the affinity mask, capped by a cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
-def _compare(img8, img32, rows, ref):
-    d = np.abs(img8[rows].astype(np.int16) - ref["rgba8"].astype(np.int16))
-    assert d.max() <= 1, f"RGBA8 max |delta| {d.max()}, {(d.max(-1) > 1).sum()} pixels over 1"
-    a, b = img32[rows], ref["rgba32f"]
-    na, nb = np.isnan(a), np.isnan(b)
-    np.testing.assert_array_equal(na, nb)
-    ok = ~na
-    assert np.abs(a[ok] - b[ok]).max() <= 2e-6
+def parity_report(name, img8, img32, ref) -> dict:
+    """Per-channel max |delta|, the |delta| histogram over all channels and the
+    pixels over 2 LSB, plus the RGBA32F comparison."""
+    d = np.abs(img8.astype(np.int16) - ref["rgba8"].astype(np.int16))
+    hist = np.bincount(np.minimum(d.ravel(), 3), minlength=4)
+    rep = {"frame": name, "pixels": int(d.shape[0] * d.shape[1]),
+           "max_abs_delta_rgba8_per_channel": [int(x) for x in d.reshape(-1, 4).max(0)],
+           "abs_delta_histogram": {"0": int(hist[0]), "1": int(hist[1]), "2": int(hist[2]),
+                                   ">2": int(hist[3])},
+           "pixels_over_1": int((d.max(-1) > 1).sum()),
+           "pixels_over_2": int((d.max(-1) > 2).sum())}
+    if img32 is not None:
+        a, b = img32, ref["rgba32f"]
+        na, nb = np.isnan(a), np.isnan(b)
+        ok = ~(na | nb)
+        rep["nan_mask_equal"] = bool(np.array_equal(na, nb))
+        rep["nan_values"] = int(na.sum())
+        rep["max_abs_delta_rgba32f"] = float(np.abs(a[ok] - b[ok]).max()) if ok.any() else 0.0
+    print(json.dumps(rep))
+    path = os.environ.get("RM_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rep) + "\n")
+    return rep
 
 
-@pytest.mark.parametrize("cfg", [(3840, 2160, 3, [0, 61, 119]), (3840, 2160, 5, [30, 90])],
-                         ids=["cfg3-4K-b3", "cfg4-4K-b5"])
-def test_production_kernel_full_size_vs_oracle(rm, oracle, gpu, cfg):
-    W, H, b, frames = cfg
+def _check(rep):
+    assert max(rep["max_abs_delta_rgba8_per_channel"]) <= 1, rep
+    if "nan_mask_equal" in rep:
+        assert rep["nan_mask_equal"], rep
+        assert rep["max_abs_delta_rgba32f"] <= 2e-6, rep
+
+
+# (name, W, H, bounces, AA, shadow, frames); frame -1 = the default frame D
+CASES = [
+    ("cfg1-512-hard", 512, 512, 0, False, 1, [-1, 60]),
+    ("cfg2-1080p-b1", 1920, 1080, 1, False, 0, [0, 119]),
+    ("cfg3-4K-b3", 3840, 2160, 3, True, 0, [0, 61, 119]),
+    ("cfg4-4K-b5", 3840, 2160, 5, True, 0, [90]),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_production_kernel_whole_frames_vs_oracle(rm, oracle, gpu, case):
+    name, W, H, b, aa, shadow, frames = case
+    nt = _host_threads()
     with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
         for f in frames:
-            u = rm.sweep_uniforms(f, 120, b, True, rm.RM_SHADOW_SOFT)
+            u = rm.sweep_uniforms(f, 120, b, aa, shadow)
             r.dispatch(u)
             img8, img32 = r.read_rgba8(), r.read_rgba32f()
-            rows = _rows(H, 40, seed=f)
-            ref = oracle.render(u, W, H, rows=rows, want_counts=False)
-            _compare(img8, img32, rows, ref)
+            ref = oracle.render(u, W, H, nthreads=nt, want_counts=False)
+            _check(parity_report(f"{name} frame {'D' if f < 0 else f}", img8, img32, ref))
 
 
 def test_cfg5_graph_replay_8k_vs_dispatch_and_oracle(rm, oracle, gpu):
     """BASELINE cfg 5: 7680x4320, 3 bounces, 4x supersampling, animated sweep
     replayed from the captured hipGraph (rm_graph_dispatch).  Every frame equals a
-    plain rm_dispatch render byte for byte and an oracle row sample within the
-    parity bars."""
+    plain rm_dispatch render byte for byte; the last one is checked against the
+    oracle on every pixel."""
     W, H = 7680, 4320
     frames = [0, 37, 74, 119]
     outs = rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F
@@ -65,6 +106,5 @@ def test_cfg5_graph_replay_8k_vs_dispatch_and_oracle(rm, oracle, gpu):
             np.testing.assert_array_equal(g8, p8)
             g32 = g.read_rgba32f()
             np.testing.assert_array_equal(g32.view(np.uint32), p.read_rgba32f().view(np.uint32))
-            rows = _rows(H, 24, seed=1000 + f)
-            ref = oracle.render(u, W, H, rows=rows, want_counts=False)
-            _compare(g8, g32, rows, ref)
+        ref = oracle.render(u, W, H, nthreads=_host_threads(), want_counts=False)
+        _check(parity_report(f"cfg5-8K-b3 frame {frames[-1]} (graph)", g8, g32, ref))

@@ -1,57 +1,40 @@
-"""The multi-GPU step of bench.py, rehearsed on one GPU: N virtual ranks render
-their row-block shards of consecutive frames with several frames in flight
-(one context and stream per in-flight frame), a `comm` stream gathers the
-shards (device copies standing in for the RCCL gather) and assembles each frame
-(rm_unshard_rgba8), all ordered only by events.  Every assembled frame must
-equal a plain full-frame render."""
+"""bench.py's N > 1 step with frames in flight, through the product path.
+
+Each in-flight frame has its own context, stream and RCCL communicator
+(rm_comm_init); rm_dispatch renders the shard, gathers it to rank 0 (ncclGather)
+and assembles the frame (k_unshard), all inside librm on the context's stream, and
+consecutive frames overlap on the contexts' streams exactly as in bench.py.  This
+box has one GPU, so the communicators have one rank (RCCL refuses two ranks on one
+device); the N-rank row-block geometry of the assembly is covered by
+tests/test_gpu_api.py (N in {2, 3, 8}) and tests/test_shard.py (gloo, world size 2).
+Every assembled frame must equal a plain one-GPU render byte for byte.
+"""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("N,nfl", [(2, 2), (4, 3), (8, 4)])
-def test_inflight_sharded_frames_assemble(rm, gpu, N, nfl):
-    import torch
-    W, H, R, F = 160, 90, 8, 7
-    us = [rm.sweep_uniforms(9 * f, 120, 3, True, 0) for f in range(F)]
-    cap = rm.shard_rows_cap(H, R, N)
-    streams = [[torch.cuda.Stream() for _ in range(nfl)] for _ in range(N)]
-    rs = [[rm.Renderer(W, H, row_block=R, shard=k, nshards=N) for _ in range(nfl)]
-          for k in range(N)]
-    outs = [[torch.zeros((cap, W, 4), dtype=torch.uint8, device="cuda") for _ in range(nfl)]
-            for _ in range(N)]
-    for k in range(N):
-        for j in range(nfl):
-            rs[k][j].set_stream(streams[k][j].cuda_stream)
-            rs[k][j].set_output_rgba8(outs[k][j].data_ptr())
-    comm = torch.cuda.Stream()
-    ru = rm.Renderer(W, H, row_block=R, shard=0, nshards=N)
-    ru.set_stream(comm.cuda_stream)
-    gathered = torch.zeros((N, cap, W, 4), dtype=torch.uint8, device="cuda")
-    frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(F)]
-    render_done = [[torch.cuda.Event() for _ in range(nfl)] for _ in range(N)]
-    gather_done = [torch.cuda.Event() for _ in range(nfl)]
-    for ev in gather_done:
-        ev.record(comm)
+@pytest.mark.parametrize("nfl,graph", [(2, False), (4, False), (4, True)])
+def test_inflight_comm_contexts_assemble(rm, gpu, nfl, graph):
+    W, H, R, F = 160, 90, 8, 9
+    us = [rm.sweep_uniforms(13 * f, 120, 3, True, 0) for f in range(F)]
+    rs = [rm.Renderer(W, H, row_block=R, shard=0, nshards=1) for _ in range(nfl)]
+    for r in rs:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        if graph:
+            r.graph_enable(True)
+    got = {}
     for f in range(F):
-        j = f % nfl
-        for k in range(N):
-            streams[k][j].wait_event(gather_done[j])
-            rs[k][j].dispatch(us[f])
-            render_done[k][j].record(streams[k][j])
-        with torch.cuda.stream(comm):
-            for k in range(N):
-                comm.wait_event(render_done[k][j])
-                gathered[k].copy_(outs[k][j])
-            ru.unshard_rgba8(gathered.data_ptr(), frames[f].data_ptr())
-            gather_done[j].record(comm)
-    torch.cuda.synchronize()
+        r = rs[f % nfl]
+        if f >= nfl:  # the context's previous frame is complete before its buffers are reused
+            got[f - nfl] = r.read_rgba8()
+        (r.graph_dispatch if graph else r.dispatch)(us[f])
+    for f in range(F - nfl, F):
+        got[f] = rs[f % nfl].read_rgba8()
     with rm.Renderer(W, H) as full:
         for f in range(F):
             full.dispatch(us[f])
-            np.testing.assert_array_equal(frames[f].cpu().numpy(), full.read_rgba8(), err_msg=f"frame {f}")
-    for row in rs:
-        for r in row:
-            r.close()
-    ru.close()
+            np.testing.assert_array_equal(got[f], full.read_rgba8(), err_msg=f"frame {f}")
+    for r in rs:
+        r.close()

@@ -9,7 +9,12 @@
 int main(int argc, char** argv) {
   const int W = 3840, H = 2160;
   const int nsh = argc > 1 ? atoi(argv[1]) : 1;  // optional: row-block shards (rank 0's shard)
-  rm_config cfg = {W, H, 0, RM_OUT_RGBA8, RM_KERNEL_PIXEL, 0, nsh > 1 ? 8 : 0, 0, nsh};
+  rm_config cfg;
+  rm_config_init(&cfg, W, H);
+  cfg.device = 0;
+  cfg.kernel = RM_KERNEL_PIXEL;
+  cfg.row_block = nsh > 1 ? 8 : 0;
+  cfg.nshards = nsh;
   rm_ctx* c;
   if (rm_create(&c, &cfg)) return 1;
   int rows = H;
