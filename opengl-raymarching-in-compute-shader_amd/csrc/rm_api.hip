@@ -52,6 +52,7 @@ struct rm_ctx {
   uint32_t* d_counts = nullptr;
   unsigned long long* d_counters = nullptr;
   float* d_uv = nullptr;          // per-column / per-row uv table (Frame::uvx / uvy)
+  bool uv_exact = false;          // lane_uv's arithmetic equals the table (uv_exact_check)
   uint32_t* d_scene = nullptr;    // runtime scene table (rm_set_scene), compiled words
   int nprims = 0;                 // 0: the built-in scene and its specialised kernel
   std::vector<rm_primitive> scene;     // the table as given (rm_get_scene)
@@ -433,6 +434,14 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.persp = 45.0f * static_cast<float>(0.01745329251994329576923690768489);
   F.uvx = c->d_uv;
   F.uvy = c->d_uv + (size_t)5 * c->cfg.width;
+  F.uv_exact = c->uv_exact ? 1 : 0;
+  const float uv_ox[4] = {0.25f, 0.75f, 0.25f, 0.75f}, uv_oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
+  for (int a = 0; a < 2; ++a) {
+    const float n = (float)(a ? c->cfg.height : c->cfg.width);
+    F.uv_dims[a] = n;
+    F.uv_rcp[a] = 1.0f / n;
+    for (int k = 0; k < 4; ++k) F.uv_off[a][k] = (a ? uv_oy[k] : uv_ox[k]) / n;
+  }
   F.bounces = u.bounceVar;
   F.aa = u.AA ? 1 : 0;
   F.width = c->cfg.width;
@@ -821,6 +830,18 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
         v += (col ? ox[k] : oy[k]) / (float)n;
         uv[(size_t)p * 5 + 1 + k] = v;
       }
+    }
+    // lane_uv (rm_scene.hpp) may form the same values arithmetically when, for every
+    // column and row, RN(1/n)-times-a plus one fma remainder correction equals the
+    // IEEE (2p - n) / n; the offsets' adds are the table's own operations
+    c->uv_exact = true;
+    for (int p = 0; p < W + H && c->uv_exact; ++p) {
+      const bool col = p < W;
+      const int i = col ? p : p - W, n = col ? W : H;
+      const float a = (float)(i * 2 - n), nf = (float)n, r = 1.0f / nf;
+      const float q0 = a * r;
+      const float q = std::fma(std::fma(-q0, nf, a), r, q0);
+      c->uv_exact = q == uv[(size_t)p * 5] && std::signbit(q) == std::signbit(uv[(size_t)p * 5]);
     }
     if ((e = hipMalloc(&c->d_uv, uv.size() * sizeof(float))) != hipSuccess ||
         (e = hipMemcpy(c->d_uv, uv.data(), uv.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)

@@ -247,6 +247,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 template <bool COUNT, bool HAVE_C0>
 __device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
   if (COUNT) c.normals++;
+  RM_STAT(27);
   float vx, vy, vz;
   normal_samples<HAVE_C0>(pos, F.blend, F.omblend, c0, vx, vy, vz);
 #ifdef RM_DBL_NORMAL
@@ -273,6 +274,7 @@ template <bool COUNT>
 __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   float res = 1.0f, t = 0.0f;
   int dummy;
+  RM_STAT(29);
   const float ex = shadow_exit_init(F.k, ro, rd);
   for (int i = 0; i < 16; ++i) {
     if (lin_exit(ex, t)) {  // the remaining steps are no-ops
@@ -300,6 +302,7 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     // After a MATTE prevObject every remaining iteration is a colour no-op
     // (glsl:181,189-190): stop instead of running the dead marches.
     if (prevMatte) break;
+    RM_STAT(26);
     rayDir = reflect(rayDir, normal);
     int id;
     f3 tcol;
@@ -348,7 +351,9 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     th = (th2 == th) ? th : __builtin_nanf("");
   }
 #endif
+  RM_STAT(30);
   if (th != -1.0f) {
+    RM_STAT(31);
     f3 pos = add(ro, muls(rd, th));
     f3 normal = get_normal<COUNT, true>(F, pos, c, dl);
     if (COUNT) c.lights++;
@@ -399,7 +404,7 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
   float o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
   if (py >= 0) {
     f3 ro, rd;
-    cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
+    cast_ray(F, lane_uv(F, 0, px, -1), lane_uv(F, 1, py, -1), ro, rd);
     if (COUNT) c.rays++;
     f3 col = render<COUNT>(F, ro, rd, c);
     o0 = col.x;
@@ -446,7 +451,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
 #endif
   if (py >= 0) {
     f3 ro, rd;
-    cast_ray(F, F.uvx[px * 5 + 1 + s], F.uvy[py * 5 + 1 + s], ro, rd);
+    cast_ray(F, lane_uv(F, 0, px, s), lane_uv(F, 1, py, s), ro, rd);
     if (COUNT) c.rays++;
     col = render<COUNT>(F, ro, rd, c);
   }

@@ -84,6 +84,14 @@ struct Frame {
   // offsets offset[0..s] / dims; 5 floats per column (uvx) and per row (uvy)
   const float* uvx;
   const float* uvy;
+  // The same uv from arithmetic (lane_uv), when the host has checked that it is
+  // exact for every column and row of this frame size (uv_exact): the division
+  // (2p - dims) / dims as a multiply by RN(1 / dims) plus one fma remainder
+  // correction, and the cumulative offsets RN(offset_k / dims) added in order.
+  float uv_rcp[2];       // RN(1 / W), RN(1 / H)
+  float uv_dims[2];      // W, H as floats
+  float uv_off[2][4];    // RN(ox_k / W), RN(oy_k / H)
+  int32_t uv_exact;
   int32_t bounces; // bounceVar, 0..5
   int32_t aa;      // AA
   int32_t width, height;
@@ -704,6 +712,29 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
 
 __device__ __forceinline__ f3 gamma(f3 c) {
   return mk(gpow(c.x, 0.4545f), gpow(c.y, 0.4545f), gpow(c.z, 0.4545f));
+}
+
+// uv of pixel column (axis 0) / row (axis 1) p, sample s (-1: no supersampling):
+// glsl:301-305 and the cumulative sub-sample offsets of :309-332.  With
+// F.uv_exact the host has checked, for every p of this frame size, that the
+// fma-corrected product below equals the IEEE division (2p - n) / n
+// (rm_api.hip uv_exact_check); otherwise the host-built table is read.
+__device__ __forceinline__ float lane_uv(const Frame& F, int axis, int p, int s) {
+#ifdef RM_UV_COMPUTE
+  if (F.uv_exact) {
+    const float a = (float)(2 * p - (axis ? F.height : F.width));
+    const float r = F.uv_rcp[axis], n = F.uv_dims[axis];
+    const float q0 = a * r;
+    float v = __builtin_fmaf(__builtin_fmaf(-q0, n, a), r, q0);
+    if (s >= 0) {
+      const float v1 = v + F.uv_off[axis][0], v2 = v1 + F.uv_off[axis][1], v3 = v2 + F.uv_off[axis][2];
+      const float v4 = v3 + F.uv_off[axis][3];
+      v = s == 0 ? v1 : s == 1 ? v2 : s == 2 ? v3 : v4;
+    }
+    return v;
+  }
+#endif
+  return (axis ? F.uvy : F.uvx)[p * 5 + 1 + s];
 }
 
 // castRay glsl:68-74 over vec4 (w included, as the GLSL does).

@@ -697,7 +697,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F)
     return;
   }
   f3 ro, rd;
-  cast_ray(F, F.uvx[px * 5], F.uvy[py * 5], ro, rd);
+  cast_ray(F, lane_uv(F, 0, px, -1), lane_uv(F, 1, py, -1), ro, rd);
   if (COUNT) c.rays++;
   const f3 col = trender<COUNT, KL>(F, S, ro, rd, c);
   store_pixel(F, idx, col.x, col.y, col.z, 1.0f);
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F
   f3 col = mk(0.0f, 0.0f, 0.0f);
   if (py >= 0) {
     f3 ro, rd;
-    cast_ray(F, F.uvx[px * 5 + 1 + s], F.uvy[py * 5 + 1 + s], ro, rd);
+    cast_ray(F, lane_uv(F, 0, px, s), lane_uv(F, 1, py, s), ro, rd);
     if (COUNT) c.rays++;
     col = trender<COUNT, KL>(F, S, ro, rd, c);
   }

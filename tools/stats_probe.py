@@ -29,7 +29,9 @@ h = list(h)
 nm = {0: "cull-sdf(shadow)", 1: "lazy-retests", 2: "shadow-steps", 6: "refl-iters",
       8: "lazy-sdf", 9: "lazy-block", 10: "eval-sph0", 11: "eval-sph1", 12: "eval-blend",
       13: "eval-torus", 14: "eval-capsule", 15: "prim-iters", 16: "retest-sph0",
-      17: "retest-sph1", 18: "retest-blend", 19: "retest-torus", 20: "retest-capsule"}
+      17: "retest-sph1", 18: "retest-blend", 19: "retest-torus", 20: "retest-capsule",
+      26: "bounce-iters", 27: "normals", 29: "shadows", 30: "render-after-march",
+      31: "primary-hit-shade"}
 waves = (W * H * (4 if aa else 1) + 63) // 64
 print(f"cfg {cfg} frame {frame}: {waves} waves")
 print("%-20s %12s %14s %8s %8s" % ("point", "waves", "lanes", "lanes/w", "per wave"))
