@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build a librm variant with extra -D flags for A/B timing (tools/probe_variants.sh).
+# Build a librm variant with extra -D flags for A/B timing (tools/ab_kernel.py).
 #   tools/build_variant.sh NAME [-DFOO=1 ...]   -> tools/variants/librm_NAME.so
 #   tools/build_variant.sh NAME --rev GITREV    -> librm built from a committed revision
 #   tools/build_variant.sh NAME --patch F.diff  -> librm built with a patch applied
