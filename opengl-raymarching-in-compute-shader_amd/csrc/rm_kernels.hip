@@ -133,6 +133,9 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
         if (live) {
           float tp = t;
           for (int i = ib;; ++i) {
+#ifdef RM_WAVE_STATS
+            RM_STAT(reflected ? 6 : 15);
+#endif
             const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
             bool ex = d < 0.000001f * t;
             dl = d;

@@ -151,6 +151,20 @@ __device__ unsigned long long g_stats[64];
       atomicAdd(&g_stats[32 + (k)], (unsigned long long)__popcll(m_)); \
     }                                                                \
   } while (0)
+#elif defined(RM_WAVE_STATS)
+// Diagnostic build only (tools/wave_timeline.hip): per-wave counts of the same
+// points, g_wave_stats[32 w + k] for the wave of tile w (k_sample's tile order).
+__device__ unsigned long long* g_wave_stats;
+__device__ __forceinline__ int tile_row(int b, int n);
+__device__ __forceinline__ int tile_col(int b, int gx, int G);
+#define RM_STAT(k)                                                                             \
+  do {                                                                                         \
+    const unsigned long long m_ = __ballot(1);                                                 \
+    if (__lane_id() == __builtin_ffsll(m_) - 1) {                                              \
+      const size_t w_ = (size_t)tile_row(blockIdx.y, gridDim.y) * gridDim.x + tile_col(blockIdx.x, gridDim.x, 8); \
+      atomicAdd(&g_wave_stats[32 * w_ + (k)], 1ull);                                           \
+    }                                                                                          \
+  } while (0)
 #else
 #define RM_STAT(k) \
   do {             \

@@ -1,6 +1,7 @@
 // Diagnostic: per-wave lifetimes of one cfg-3 k_sample launch (RM_WAVE_TIMES):
 // concurrency over time (waves alive / 8 per SIMD), dispatch gaps, tail.
 #define RM_WAVE_TIMES 1
+#define RM_WAVE_STATS 1
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_kernels.hip"
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_api.hip"
 #include <algorithm>
@@ -25,15 +26,20 @@ int main(int argc, char** argv) {
   hipMalloc(&d, nw * 3 * 8);
   hipMemset(d, 0, nw * 3 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_wave_times), &d, sizeof d);
+  unsigned long long* ds;  // per-wave counts of the RM_STAT points (RM_WAVE_STATS)
+  hipMalloc(&ds, nw * 32 * 8);
+  hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_wave_stats), &ds, sizeof ds);
   rm_uniforms u;
   rm_sweep_uniforms(30, 120, 3, 1, 0, &u);
   rm_set_uniforms(c, &u);
   rm_dispatch(c);  // warm
   rm_synchronize(c);
+  hipMemset(ds, 0, nw * 32 * 8);
   rm_dispatch(c);
   rm_synchronize(c);
-  std::vector<unsigned long long> h(nw * 3);
+  std::vector<unsigned long long> h(nw * 3), hs(nw * 32);
   hipMemcpy(h.data(), d, nw * 3 * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(hs.data(), ds, nw * 32 * 8, hipMemcpyDeviceToHost);
   unsigned long long t0 = ~0ull, t1 = 0;
   for (size_t w = 0; w < nw; ++w) { t0 = std::min(t0, h[3 * w]); t1 = std::max(t1, h[3 * w + 1]); }
   const double span = (double)(t1 - t0);  // wall_clock64 ticks (100 MHz)
@@ -72,11 +78,27 @@ int main(int argc, char** argv) {
   for (size_t w = 0; w < nw; ++w) ends.push_back({h[3 * w + 1], w});
   std::sort(ends.begin(), ends.end());
   const size_t gx = W / 4;
-  printf("last 12 waves to finish (tile row of %d, col, start us, life us):\n", (rows + 3) / 4);
+  printf("last 12 waves to finish (tile row of %d, col, start us, life us; wave-level counts of "
+         "primary steps, reflected steps, lazy blocks, re-tests, shadow steps, bounce iterations, "
+         "normals, shadows):\n", (rows + 3) / 4);
+  auto counts = [&](size_t w) {
+    const unsigned long long* q = &hs[32 * w];
+    printf("  prim %llu refl %llu blk %llu rt %llu sh %llu bnc %llu nrm %llu shd %llu", q[15], q[6], q[9], q[1],
+           q[2], q[26], q[27], q[29]);
+  };
   for (size_t i = nw - 12; i < nw; ++i) {
     const size_t w = ends[i].second;
-    printf("  row %4zu col %4zu start %7.1f life %6.1f\n", w / gx, w % gx, (h[3 * w] - t0) / 100.0,
+    printf("  row %4zu col %4zu start %7.1f life %6.1f", w / gx, w % gx, (h[3 * w] - t0) / 100.0,
            (h[3 * w + 1] - h[3 * w]) / 100.0);
+    counts(w);
+    printf("\n");
+  }
+  {  // the mean wave for comparison
+    std::vector<double> m(32, 0.0);
+    for (size_t w = 0; w < nw; ++w)
+      for (int k = 0; k < 32; ++k) m[k] += (double)hs[32 * w + k] / nw;
+    printf("mean wave: prim %.1f refl %.1f blk %.1f rt %.1f sh %.1f bnc %.2f nrm %.2f shd %.2f\n", m[15], m[6], m[9],
+           m[1], m[2], m[26], m[27], m[29]);
   }
   // lifetime by tile-row band (10 bands)
   for (int b = 0; b < 10; ++b) {
