@@ -40,6 +40,26 @@ $(PKG)/build/%.o: $(CSRC)/%.hip $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# rm_kernels.hip is built twice: k_pixel + k_unshard (rm_kernels.o),
+# and k_sample alone without SLP vectorisation (rm_kernels_aa.o): pairing its f32
+# adds / muls into packed v_pk_* ops costs register moves to form the pairs and
+# measured 3.9 % slower per cfg3 frame; k_pixel keeps SLP.  Both at -O2, which
+# measured 0.4-2 % faster than -O3 for each (round 3, profiles/r03_compiler_ab.txt).
+KFLAGS   := $(HIPFLAGS) -O2
+$(PKG)/build/rm_kernels.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(KFLAGS) -DRM_KERNELS_PIXEL_ONLY -c $< -o $@
+
+$(PKG)/build/rm_kernels_aa.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(KFLAGS) -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c $< -o $@
+
+# the scene-table kernels without SLP vectorisation too (generic -2.7 %, the
+# hiprtc-specialised ones get the same flag in rm_jit.hip: -6.5 % per cfg3 frame)
+$(PKG)/build/rm_table.o: $(CSRC)/rm_table.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -fno-slp-vectorize -c $< -o $@
+
 $(PKG)/build/rm_jit_src.inc: $(CSRC)/rm_table.hip $(RM_HDRS) $(PKG)/tools/embed_sources.py
 	@mkdir -p $(dir $@)
 	python3 $(PKG)/tools/embed_sources.py $@ $(JIT_SRCS)
@@ -57,7 +77,7 @@ $(PKG)/build/rm_comm.o: $(CSRC)/rm_comm.cpp $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_table.o $(PKG)/build/rm_jit.o $(PKG)/build/rm_host.o $(PKG)/build/rm_comm.o
+$(LIBRM): $(PKG)/build/rm_api.o $(PKG)/build/rm_kernels.o $(PKG)/build/rm_kernels_aa.o $(PKG)/build/rm_table.o $(PKG)/build/rm_jit.o $(PKG)/build/rm_host.o $(PKG)/build/rm_comm.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lhiprtc -ldl
 
 $(ORACLE): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h

@@ -458,9 +458,20 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
     if (COUNT) c.rays++;
     col = render<COUNT>(F, ro, rd, c);
   }
+#ifdef RM_DPP_AA
+  // the quad's other samples by DPP quad permutes (lane s = 0 reads lanes 1, 2, 3
+  // of its quad): VALU moves instead of LDS permutes
+  auto q1 = [](float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x39, 0xf, 0xf, false)); };
+  auto q2 = [](float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false)); };
+  auto q3 = [](float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x93, 0xf, 0xf, false)); };
+  const float r1 = q1(col.x), g1 = q1(col.y), b1 = q1(col.z);
+  const float r2 = q2(col.x), g2 = q2(col.y), b2 = q2(col.z);
+  const float r3 = q3(col.x), g3 = q3(col.y), b3 = q3(col.z);
+#else
   const float r1 = __shfl(col.x, lane + 1), g1 = __shfl(col.y, lane + 1), b1 = __shfl(col.z, lane + 1);
   const float r2 = __shfl(col.x, lane + 2), g2 = __shfl(col.y, lane + 2), b2 = __shfl(col.z, lane + 2);
   const float r3 = __shfl(col.x, lane + 3), g3 = __shfl(col.y, lane + 3), b3 = __shfl(col.z, lane + 3);
+#endif
   uint32_t cnt = 0;
   if (COUNT) {
     const uint32_t mine = c.march + c.reflect + c.shadow + 4u * c.normals;
@@ -497,14 +508,22 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
 // Entry points: the frame constants by value (kernel arguments in SGPRs).
 // 64 VGPRs: 8 waves per SIMD, the most a SIMD holds (the kernels are latency
 // bound; 7 and 6 waves measured slower).
+#ifndef RM_KERNELS_AA_ONLY
 template <bool COUNT>
 __global__ __launch_bounds__(64, 8) void k_pixel(Frame F) {
   pixel_body<COUNT>(F);
 }
+#endif
+#ifndef RM_KERNELS_PIXEL_ONLY
+// Built in its own object without SLP vectorisation (Makefile): pairing
+// independent f32 adds / muls into v_pk_add_f32 / v_pk_mul_f32 costs register
+// moves to form the pairs and measured 3.5 % slower per cfg3 frame (round 3,
+// profiles/r03_ab_noslp.txt); k_pixel keeps it (2 % faster with it, cfg2).
 template <bool COUNT>
 __global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
   sample_body<COUNT>(F);
 }
+#endif
 
 // Reassemble [nshards][rows_cap][width] packed shard images into the frame.
 // One grid row per frame row: the source row (shard, local row) is computed once
@@ -537,31 +556,42 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
 // ---- launch wrappers used by rm_api.hip --------------------------------------
 namespace rm {
 
+#ifndef RM_KERNELS_AA_ONLY
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy) {
   *gx = aa ? (width + rmd::kSampleTileW - 1) / rmd::kSampleTileW : (width + rmd::kTileW - 1) / rmd::kTileW;
   *gy = aa ? (rows + rmd::kSampleTileH - 1) / rmd::kSampleTileH : (rows + rmd::kTileH - 1) / rmd::kTileH;
 }
+#endif
 
 // F.grid_x / grid_y must be pixel_grid(F.width, F.rows, F.aa) (make_frame): the
 // kernels read the grid from their arguments, not from the hidden dispatch
 // arguments, so the prologue's tile arithmetic waits for one round of loads.
-hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
+#ifndef RM_KERNELS_PIXEL_ONLY
+// k_sample lives in its own code object (this file built with RM_KERNELS_AA_ONLY
+// and -fno-slp-vectorize, Makefile): see the note at k_sample.
+hipError_t launch_sample(const rmd::Frame& F, bool counters, hipStream_t s) {
   const dim3 grid(F.grid_x, F.grid_y);
-  if (F.aa) {
-    if (counters)
-      hipLaunchKernelGGL(rmd::k_sample<true>, grid, dim3(64), 0, s, F);
-    else
-      hipLaunchKernelGGL(rmd::k_sample<false>, grid, dim3(64), 0, s, F);
-    return hipGetLastError();
-  }
+  if (counters)
+    hipLaunchKernelGGL(rmd::k_sample<true>, grid, dim3(64), 0, s, F);
+  else
+    hipLaunchKernelGGL(rmd::k_sample<false>, grid, dim3(64), 0, s, F);
+  return hipGetLastError();
+}
+#endif
+#ifndef RM_KERNELS_AA_ONLY
+hipError_t launch_sample(const rmd::Frame& F, bool counters, hipStream_t s);
+hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
+  if (F.aa) return launch_sample(F, counters, s);
+  const dim3 grid(F.grid_x, F.grid_y);
   if (counters)
     hipLaunchKernelGGL(rmd::k_pixel<true>, grid, dim3(64), 0, s, F);
   else
     hipLaunchKernelGGL(rmd::k_pixel<false>, grid, dim3(64), 0, s, F);
   return hipGetLastError();
 }
+#endif
 
-#ifdef RM_STATS
+#if defined(RM_STATS) && !defined(RM_KERNELS_AA_ONLY)
 // Diagnostic builds: rm_debug_stats() (rm_api.hip) reads and clears g_stats.
 hipError_t debug_stats(unsigned long long* out, bool clear) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rmd::g_stats), 64 * sizeof(unsigned long long));
@@ -573,6 +603,7 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 }
 #endif
 
+#ifndef RM_KERNELS_AA_ONLY
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s) {
   // 16-B copies need 16-B rows (width % 4 == 0) and 16-B aligned images: the
@@ -591,5 +622,6 @@ hipError_t launch_unshard(const void* gathered, void* frame, int width, int heig
                        nshards, rows_cap);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace rm

@@ -20,10 +20,15 @@ fi
 pkg=opengl-raymarching-in-compute-shader_amd
 flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$src/include $*"
 b=$(mktemp -d)
-for f in rm_api rm_kernels rm_table; do
-  [ -f "$src/$pkg/csrc/$f.hip" ] || continue
-  /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/$f.hip" -o "$b/$f.o" &
-done
+/opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_api.hip" -o "$b/rm_api.o" &
+/opt/rocm/bin/hipcc $flags -fno-slp-vectorize -c "$src/$pkg/csrc/rm_table.hip" -o "$b/rm_table.o" &
+# rm_kernels.hip as the Makefile builds it (k_sample alone, without SLP), except
+# for the RM_STATS build, whose counters must live in one code object
+case "$*" in
+  *RM_STATS*) /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" & ;;
+  *) /opt/rocm/bin/hipcc $flags -O2 -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
+     /opt/rocm/bin/hipcc $flags -O2 -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels_aa.o" & ;;
+esac
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
 [ -f "$src/$pkg/csrc/rm_comm.cpp" ] && { /opt/rocm/bin/hipcc $flags -x hip -c "$src/$pkg/csrc/rm_comm.cpp" -o "$b/rm_comm.o" & }
 if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed the table sources
