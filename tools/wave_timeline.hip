@@ -1,7 +1,8 @@
 // Diagnostic: per-wave lifetimes of one cfg-3 k_sample launch (RM_WAVE_TIMES):
 // concurrency over time (waves alive / 8 per SIMD), dispatch gaps, tail.
+// Build with -DRM_WAVE_STATS for per-wave counts of the RM_STAT points as well
+// (their atomics slow the launch ~10x: lifetimes are then only relative).
 #define RM_WAVE_TIMES 1
-#define RM_WAVE_STATS 1
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_kernels.hip"
 #include "../opengl-raymarching-in-compute-shader_amd/csrc/rm_api.hip"
 #include <algorithm>
@@ -26,9 +27,12 @@ int main(int argc, char** argv) {
   hipMalloc(&d, nw * 3 * 8);
   hipMemset(d, 0, nw * 3 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_wave_times), &d, sizeof d);
-  unsigned long long* ds;  // per-wave counts of the RM_STAT points (RM_WAVE_STATS)
+  unsigned long long* ds = nullptr;  // per-wave counts of the RM_STAT points (RM_WAVE_STATS)
   hipMalloc(&ds, nw * 32 * 8);
+  hipMemset(ds, 0, nw * 32 * 8);
+#ifdef RM_WAVE_STATS
   hipMemcpyToSymbol(HIP_SYMBOL(rmd::g_wave_stats), &ds, sizeof ds);
+#endif
   rm_uniforms u;
   rm_sweep_uniforms(30, 120, 3, 1, 0, &u);
   rm_set_uniforms(c, &u);
