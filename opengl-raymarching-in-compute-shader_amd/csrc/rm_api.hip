@@ -202,7 +202,17 @@ int comm_dead(rm_ctx* c) {
 
 // Waits until every stream of the frame's contexts has drained, polling the
 // communicators' asynchronous errors, within the context's deadline.
+int comm_wait_devs(rm_ctx* c);
+// (the caller's current device is restored: a multi-GPU context's wait visits
+// every device)
 int comm_wait(rm_ctx* c) {
+  int dev = 0;
+  const bool have_dev = hipGetDevice(&dev) == hipSuccess;
+  const int rc = comm_wait_devs(c);
+  if (have_dev) (void)hipSetDevice(dev);
+  return rc;
+}
+int comm_wait_devs(rm_ctx* c) {
   std::string err;
   const rm::Rccl* r = rm::rccl(&err);
   if (!r) return fail(c, RM_ERR_COMM, err);
@@ -474,12 +484,26 @@ void graph_release(rm_ctx* c) {
 
 void free_all(rm_ctx* c) {
   graph_release(c);
+  {
+    // the communicators of this context (its own, or its devices'), torn down
+    // together and within the deadline (rm_comm.cpp teardown)
+    std::vector<ncclComm_t> cs;
+    for (rm_ctx* m : c->subs.empty() ? std::vector<rm_ctx*>{c} : c->subs)
+      if (m->own_comm && m->comm) {
+        cs.push_back(m->comm);
+        m->comm = nullptr;
+      }
+    std::string err;
+    const rm::Rccl* r = cs.empty() ? nullptr : rm::rccl(&err);
+    if (r) {
+      int dev = 0;
+      const bool have_dev = hipGetDevice(&dev) == hipSuccess;
+      rm::teardown(r, cs.data(), (int)cs.size(), c->comm_timeout_ms);
+      if (have_dev) (void)hipSetDevice(dev);
+    }
+  }
   for (rm_ctx* s : c->subs) rm_destroy(s);
   c->subs.clear();
-  if (c->own_comm && c->comm) {
-    std::string err;
-    if (const rm::Rccl* r = rm::rccl(&err)) (void)r->CommDestroy(c->comm);
-  }
   c->comm = nullptr;
   for (void* p : {(void*)c->d_gathered, (void*)c->d_frame, (void*)c->d_gathered32, (void*)c->d_frame32,
                   (void*)c->d_rgba8, (void*)c->d_rgba32f, (void*)c->d_counts, (void*)c->d_counters,
@@ -643,7 +667,7 @@ int create_multi(rm_ctx** out, const rm_config* cfg) {
   for (int i = 0; i < n; ++i) {
     if ((rc = comm_attach(c->subs[i], comms[i], i, n, true, true)) != RM_OK) {
       c->err = c->subs[i]->err;
-      for (int j = i + 1; j < n; ++j) (void)r->CommDestroy(comms[j]);
+      for (int j = i + 1; j < n; ++j) (void)r->CommAbort(comms[j]);
       return bail(rc);
     }
     c->subs[i]->comm_timeout_ms = c->comm_timeout_ms;
@@ -1463,7 +1487,7 @@ int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
   }
   RM_HIP(c, hipStreamSynchronize(c->stream));  // frames already queued keep their buffers
   if ((rc = comm_attach(c, comm, rank, nranks, true, false)) != RM_OK) {
-    (void)r->CommDestroy(comm);
+    (void)r->CommAbort(comm);  // this rank leaves: its peers see the abort
     c->comm = nullptr;
     return rc;
   }

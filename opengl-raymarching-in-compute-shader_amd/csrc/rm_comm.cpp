@@ -41,6 +41,7 @@ void load() {
   sym("ncclGetUniqueId", g_rccl.GetUniqueId);
   sym("ncclCommInitRank", g_rccl.CommInitRank);
   sym("ncclCommInitRankConfig", g_rccl.CommInitRankConfig);
+  sym("ncclCommFinalize", g_rccl.CommFinalize);
   sym("ncclCommDestroy", g_rccl.CommDestroy);
   sym("ncclCommAbort", g_rccl.CommAbort);
   sym("ncclCommGetAsyncError", g_rccl.CommGetAsyncError);
@@ -88,6 +89,22 @@ ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long time
         std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
       return ncclInProgress;
     poll_pause(spins);
+  }
+}
+
+void teardown(const Rccl* r, ncclComm_t* comms, int n, long timeout_ms) {
+  bool ok = true;
+  for (int i = 0; i < n; ++i) {
+    if (!comms[i]) continue;
+    const ncclResult_t e = r->CommFinalize(comms[i]);
+    ok = ok && (e == ncclSuccess || e == ncclInProgress);
+  }
+  if (ok) ok = wait_ready(r, comms, n, timeout_ms) == ncclSuccess;
+  for (int i = 0; i < n; ++i) {
+    if (!comms[i]) continue;
+    if (ok) (void)r->CommDestroy(comms[i]);
+    else (void)r->CommAbort(comms[i]);
+    comms[i] = nullptr;
   }
 }
 

@@ -18,6 +18,7 @@ struct Rccl {
   decltype(&ncclGetUniqueId) GetUniqueId;
   decltype(&ncclCommInitRank) CommInitRank;
   decltype(&ncclCommInitRankConfig) CommInitRankConfig;
+  decltype(&ncclCommFinalize) CommFinalize;
   decltype(&ncclCommDestroy) CommDestroy;
   decltype(&ncclCommAbort) CommAbort;
   decltype(&ncclCommGetAsyncError) CommGetAsyncError;
@@ -46,5 +47,12 @@ ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long time
 
 // Back-off for host polling loops: yields first, then sleeps up to 1 ms.
 void poll_pause(int spins);
+
+// Tears down comms[0..n) of one process (the devices of a multi-GPU context, or
+// one rank): ncclCommFinalize on all of them first (a single-process
+// communicator is quiescent only once every device has finalized), then waits
+// for them within timeout_ms and destroys them, or aborts them all when the
+// wait fails (a dead peer cannot hang the teardown).
+void teardown(const Rccl* r, ncclComm_t* comms, int n, long timeout_ms);
 
 }  // namespace rm
