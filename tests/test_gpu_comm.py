@@ -132,7 +132,12 @@ def test_comm_init_validation(rm, gpu):
             r.comm_init(cid, 2, 0)
         assert e.value.code == rm.RM_ERR_INVALID
     with rm.Renderer(32, 32) as r:
+        r.comm_check()  # no communicator: healthy
+        with pytest.raises(rm.RMError) as e:
+            r.comm_set_timeout(-1)
+        assert e.value.code == rm.RM_ERR_INVALID
         r.comm_init(cid, 1, 0)
+        r.comm_check()
         with pytest.raises(rm.RMError) as e:
             r.comm_init(cid, 1, 0)
         assert e.value.code == rm.RM_ERR_STATE
