@@ -518,7 +518,7 @@ __global__ __launch_bounds__(64, 8) void k_pixel(Frame F) {
 // Built in its own object without SLP vectorisation (Makefile): pairing
 // independent f32 adds / muls into v_pk_add_f32 / v_pk_mul_f32 costs register
 // moves to form the pairs and measured 3.5 % slower per cfg3 frame (round 3,
-// profiles/r03_ab_noslp.txt); k_pixel keeps it (2 % faster with it, cfg2).
+// profiles/r03_compiler_ab.txt); k_pixel keeps it (1-2 % faster with it, cfg2).
 template <bool COUNT>
 __global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
   sample_body<COUNT>(F);
