@@ -60,6 +60,10 @@ using rm::TABLE_WORDS;
 // Wave vote on the ballot builtin itself (hiprtc's __any widens the predicate
 // to an int and compares it again: two extra VALU per vote).
 __device__ __forceinline__ bool wany(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+// A table word every lane reads alike, in a scalar register.
+__device__ __forceinline__ float uword(const float* p) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(*p)));
+}
 
 // Correctly rounded sqrt of a sum of squares (x >= 0, +inf or NaN).  The fast
 // form is sqrt_cr_nonneg (exact on [0, FLT_MAX], rm_fastmath.hpp) with +inf
@@ -118,10 +122,25 @@ struct Table {
   static constexpr int n = RM_TS_N;
 #else
   int n;
+  // The fast plane (generic kernel): the table's only plane when it has exactly
+  // one (the reference's floor, and most scenes), with its parameters in scalar
+  // registers from staging on, so the every-step plane evaluation needs no LDS
+  // reads, no type dispatch and no entry loop (plane_fast: prim_dist's plane
+  // arithmetic, the same float operations).  fp = -1: none.
+  int fp;
+  float fpc[3], fpn[3], fpw;
+  int fpswz;
 #endif
   float blend, omblend;
 
   __device__ __forceinline__ const float* exits() const { return t + n * TABLE_WORDS; }
+#ifndef RM_TABLE_STATIC
+  __device__ __forceinline__ float plane_fast(f3 p) const {
+    f3 q = sub(p, mk(fpc[0], fpc[1], fpc[2]));
+    if (fpswz == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
+    return dot(q, mk(fpn[0], fpn[1], fpn[2])) + fpw;
+  }
+#endif
 
   __device__ __forceinline__ const float* entry(int k) const { return t + k * TABLE_WORDS; }
   __device__ __forceinline__ int type(int k) const {
@@ -233,6 +252,12 @@ struct Table {
   // there changes neither d nor best: no per-lane mask tests (exec-masked
   // lanes would cost the same cycles).
   __device__ __forceinline__ float dist_mask(f3 p, uint32_t wave, int& best) const {
+#ifndef RM_TABLE_STATIC
+    if (fp >= 0 && wave == (1u << fp)) {  // opU(+inf, v) = v (dist_mask's first take)
+      best = fp;
+      return plane_fast(p);
+    }
+#endif
     float d = __builtin_huge_valf();
     best = 0;
 #ifdef RM_TABLE_STATIC
@@ -409,8 +434,12 @@ struct TLazy {
       for (int k = 0; k < S.n; ++k)
         if (S.type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(S.entry(k), RM_PRIM_PLANE, p, S.blend, S.omblend));
 #else
-      for (uint32_t pm = __float_as_uint(ex[rm::EX_PLANE_MASK]); pm; pm &= pm - 1u)
-        U = gmin(U, prim_dist(S.entry(__builtin_ctz(pm)), RM_PRIM_PLANE, p, S.blend, S.omblend));
+      if (S.fp >= 0) {
+        U = gmin(U, S.plane_fast(p));
+      } else {
+        for (uint32_t pm = __float_as_uint(ex[rm::EX_PLANE_MASK]); pm; pm &= pm - 1u)
+          U = gmin(U, prim_dist(S.entry(__builtin_ctz(pm)), RM_PRIM_PLANE, p, S.blend, S.omblend));
+      }
 #endif
 #pragma unroll
       for (int j = 0; j < KL; ++j) {
@@ -655,6 +684,17 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
   __syncthreads();
   S.t = lds;
+  const uint32_t pm = __float_as_uint(uword(S.exits() + rm::EX_PLANE_MASK));
+  S.fp = (pm != 0 && (pm & (pm - 1u)) == 0) ? __builtin_ctz(pm) : -1;
+  if (S.fp >= 0) {
+    const float* P = S.entry(S.fp);
+    for (int j = 0; j < 3; ++j) {
+      S.fpc[j] = uword(P + rm::TW_CENTER + j);
+      S.fpn[j] = uword(P + rm::TW_P + j);
+    }
+    S.fpw = uword(P + rm::TW_P + 3);
+    S.fpswz = __float_as_int(uword(P + rm::TW_SWIZZLE));
+  }
   return S;
 #endif
 }
