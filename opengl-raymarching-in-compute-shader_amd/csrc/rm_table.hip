@@ -130,12 +130,17 @@ struct Table {
   int fp;
   float fpc[3], fpn[3], fpw;
   int fpswz;
+  bool fpaxis;  // normal (0, n_y, 0): the plane is q.y n_y + w (the specialised kernel's shortcut)
 #endif
   float blend, omblend;
 
   __device__ __forceinline__ const float* exits() const { return t + n * TABLE_WORDS; }
 #ifndef RM_TABLE_STATIC
   __device__ __forceinline__ float plane_fast(f3 p) const {
+    // q.x n_x and q.z n_z are signed zeros for finite q: the sum is q.y n_y + w
+    // (prim_dist's RM_TABLE_STATIC shortcut, here on a uniform flag: -1.2 % per
+    // cfg3 frame; the per-lane test inside the type switch had measured +5 %)
+    if (fpaxis) return ((fpswz == RM_SWIZZLE_XZY ? p.z - fpc[2] : p.y - fpc[1])) * fpn[1] + fpw;
     f3 q = sub(p, mk(fpc[0], fpc[1], fpc[2]));
     if (fpswz == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
     return dot(q, mk(fpn[0], fpn[1], fpn[2])) + fpw;
@@ -694,6 +699,7 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
     }
     S.fpw = uword(P + rm::TW_P + 3);
     S.fpswz = __float_as_int(uword(P + rm::TW_SWIZZLE));
+    S.fpaxis = S.fpn[0] == 0.0f && S.fpn[2] == 0.0f;
   }
   return S;
 #endif
