@@ -304,3 +304,31 @@ def test_frame_phases_split_render_gather_assembly(rm, gpu):
         r.dispatch(u)
         ph = r.frame_phases()
         assert ph["render_ms"] > 0 and ph["gather_ms"] == 0 and ph["assemble_ms"] == 0
+
+
+@pytest.mark.parametrize("N", [2, 3, 8])
+def test_rgba32f_assembly_geometry_at_n_shards(rm, gpu, N):
+    """The RGBA32F frame of an N-rank gather is assembled by k_unshard as an
+    image of 4 x width 32-bit words (rm_api.hip comm_assemble).  With one GPU the
+    N-rank geometry is rehearsed directly: N sharded contexts render RGBA32F
+    shards, the shards are laid out as ncclGather leaves them on rank 0
+    ([N][rows_cap][W] float4), and the same unshard over a 4W-wide context
+    reassembles them; the frame equals a one-GPU RGBA32F render bit for bit."""
+    import torch
+    W, H, R = 160, 90, 8
+    u = _frames(rm, 1)[0]
+    cap = rm.shard_rows_cap(H, R, N)
+    shards = []
+    for k in range(N):
+        with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA32F, row_block=R, shard=k, nshards=N) as r:
+            r.dispatch(u)
+            shards.append(r.read_rgba32f())
+    gathered = torch.from_numpy(np.stack(shards)).cuda().contiguous()  # [N][cap][W][4]
+    frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # torch's stream is not ordered with the context's
+    with rm.Renderer(4 * W, H, row_block=R, shard=0, nshards=N) as asm:
+        asm.unshard_rgba8(gathered.data_ptr(), frame.data_ptr())
+        asm.synchronize()
+    want = _reference32(rm, W, H, [u])[0][1]
+    assert gathered.shape[1] == cap
+    np.testing.assert_array_equal(frame.cpu().numpy().view(np.uint32), want.view(np.uint32))
