@@ -1,13 +1,15 @@
 """Render-only throughput of rank 0's shard at N = 1, 2, 4, 8 (cfg 3) with
 1..4 frames in flight (separate contexts and streams): what the multi-GPU step
 can reach before the gather."""
-import json, sys, time
+import json, os, sys, time
 sys.path.insert(0, 'opengl-raymarching-in-compute-shader_amd')
 import torch
 import rmarch as rm
 W, H, K = 3840, 2160, 24
-for N in (1, 2, 4, 8):
-    for nfl in (1, 2, 3, 4):
+NS = [int(x) for x in os.environ.get("PROBE_N", "1,2,4,8").split(",")]
+NFL = [int(x) for x in os.environ.get("PROBE_NFL", "1,2,3,4").split(",")]
+for N in NS:
+    for nfl in NFL:
         streams = [torch.cuda.Stream() for _ in range(nfl)]
         kw = dict(row_block=8, shard=0, nshards=N) if N > 1 else {}
         rs = [rm.Renderer(W, H, **kw) for _ in range(nfl)]
