@@ -130,6 +130,7 @@ struct Table {
   int fp;
   float fpc[3], fpn[3], fpw;
   int fpswz;
+  const float* sb;  // the lazy slots' balls, 4 words each (centre, radius), slot order, in LDS
   bool fpaxis;  // normal (0, n_y, 0): the plane is q.y n_y + w (the specialised kernel's shortcut)
 #endif
   float blend, omblend;
@@ -450,7 +451,14 @@ struct TLazy {
       for (int j = 0; j < KL; ++j) {
         if (j < ns && wany(!(t < te[j]))) {
           const int k = (int)ex[rm::EX_SLOTS + j];
+#ifndef RM_TABLE_STATIC
+          // the slot's ball gathered at staging: one 16-byte LDS read (-0.9 / -1.9 %
+          // per cfg3 / cfg2 frame against its four words read through the entry)
+          const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];
+          const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+#else
           const float* B = S.entry(k) + rm::TW_BALL;
+#endif
           const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
           const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
                                           1.0f - 0x1p-12f, -B[3]);
@@ -689,6 +697,16 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   for (int i = threadIdx.x; i < (int)rm::scene_words(F.nprims); i += blockDim.x) lds[i] = F.scene[i];
   __syncthreads();
   S.t = lds;
+  {
+    // the slots' balls gathered after the table (16-byte aligned): lane l copies
+    // word l % 4 of slot l / 4's ball
+    const int nw = (int)rm::scene_words(F.nprims);
+    float* sb = lds + ((nw + 3) & ~3);
+    const int l = threadIdx.x, ns = (int)S.exits()[rm::EX_NSLOTS];
+    if (l < 4 * ns) sb[l] = S.entry((int)S.exits()[rm::EX_SLOTS + l / 4])[rm::TW_BALL + l % 4];
+    __syncthreads();
+    S.sb = sb;
+  }
   const uint32_t pm = __float_as_uint(uword(S.exits() + rm::EX_PLANE_MASK));
   S.fp = (pm != 0 && (pm & (pm - 1u)) == 0) ? __builtin_ctz(pm) : -1;
   if (S.fp >= 0) {
@@ -804,7 +822,8 @@ namespace rm {
 namespace {
 template <int KL>
 void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
-  const size_t lds = rm::scene_words(F.nprims) * sizeof(float);
+  // the table, then the lazy slots' balls (Table::sb)
+  const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
   if (F.aa) {
     const dim3 g((F.width + 3) / 4, (F.rows + 3) / 4);
     if (counters)
