@@ -24,6 +24,10 @@
 // For the reference scene (rm_default_scene) the image equals the built-in
 // kernel's bit for bit (tests/test_gpu_scene.py); other tables are checked
 // against the oracle's table mode (oracle/rm_oracle.c rmo_render_scene).
+//
+// Diagnostic builds only: RM_TDBL_<MARCH|BMARCH|SHADOW|NORMAL> runs that phase
+// twice (its marginal cost per frame, tools/ab_kernel.py --table / --spec; the
+// specialised kernels get the define through RM_JIT_EXTRA, rm_jit.hip).
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #endif
@@ -389,7 +393,8 @@ struct TLazy {
   const float* ex;
   int ns;
   uint32_t always;
-  float te[KL];
+  float te_[KL];
+  __device__ __forceinline__ float& te(int j) { return te_[j]; }
   float temin, sig2, sl0, inv, grow, dprev;
 
   __device__ __forceinline__ TLazy(const Table& S, f3 ro, f3 rd) {
@@ -399,7 +404,7 @@ struct TLazy {
     const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
     always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
 #pragma unroll
-    for (int j = 0; j < KL; ++j) te[j] = j < ns ? -INF : INF;
+    for (int j = 0; j < KL; ++j) te(j) = j < ns ? -INF : INF;
     temin = ns > 0 ? -INF : INF;
     const float lip = ex[rm::EX_LIP];
     sig2 = 2.0f * ex[rm::EX_SIGMA];
@@ -449,7 +454,7 @@ struct TLazy {
 #endif
 #pragma unroll
       for (int j = 0; j < KL; ++j) {
-        if (j < ns && wany(!(t < te[j]))) {
+        if (j < ns && wany(!(t < te(j)))) {
           const int k = (int)ex[rm::EX_SLOTS + j];
 #ifndef RM_TABLE_STATIC
           // the slot's ball gathered at staging: one 16-byte LDS read (-0.9 / -1.9 %
@@ -463,14 +468,14 @@ struct TLazy {
           const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
                                           1.0f - 0x1p-12f, -B[3]);
           const float g = lb - U - sl;
-          const bool expired = !(t < te[j]);
-          te[j] = __builtin_fmaxf(te[j], __builtin_fmaxf(__builtin_fmaf(g, inv, t), t));
+          const bool expired = !(t < te(j));
+          te(j) = __builtin_fmaxf(te(j), __builtin_fmaxf(__builtin_fmaf(g, inv, t), t));
           if (wany(expired && !(g > 0.0f))) wmask |= 1u << k;
         }
       }
-      temin = te[0];
+      temin = te(0);
 #pragma unroll
-      for (int j = 1; j < KL; ++j) temin = __builtin_fminf(temin, te[j]);
+      for (int j = 1; j < KL; ++j) temin = __builtin_fminf(temin, te(j));
     }
     dprev = S.dist_mask(p, wmask, best);
     return dprev;
@@ -506,10 +511,10 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
     const float d0 = prep[rm::TP_D0];
 #pragma unroll
     for (int j = 0; j < KL; ++j)
-      if (j < lz.ns) lz.te[j] = __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f);
-    lz.temin = lz.te[0];
+      if (j < lz.ns) lz.te(j) = __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f);
+    lz.temin = lz.te(0);
 #pragma unroll
-    for (int j = 1; j < KL; ++j) lz.temin = __builtin_fminf(lz.temin, lz.te[j]);
+    for (int j = 1; j < KL; ++j) lz.temin = __builtin_fminf(lz.temin, lz.te(j));
     lz.dprev = d0;
     t = d0;
     i0 = 1;
@@ -629,6 +634,14 @@ __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 
   return res;
 }
 
+// Diagnostic builds only (RM_TDBL_<PHASE>, tools/ab_kernel.py): a phase run
+// twice on an opaque copy of its input, so its marginal cost shows per frame.
+__device__ __forceinline__ float topaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ f3 topaque(f3 v) { return mk(topaque(v.x), topaque(v.y), topaque(v.z)); }
+
 // bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
 // the colour unchanged (glsl:181, 189-190): the loop stops there.
 template <bool COUNT, int KL>
@@ -641,9 +654,21 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
     if (prevMat == 0.0f) break;
     rayDir = reflect(rayDir, normal);
     THit h = tmarch<COUNT, KL>(S, add(pos, muls(normal, 0.001f)), rayDir, true, c);
+#ifdef RM_TDBL_BMARCH
+    if (!COUNT) {
+      const THit h2 = tmarch<COUNT, KL>(S, topaque(add(pos, muls(normal, 0.001f))), rayDir, true, c);
+      h.t = (h2.t == h.t) ? h.t : __builtin_nanf("");
+    }
+#endif
     pos = add(pos, muls(rayDir, h.t));
     // the normal of a miss on the last bounce is never read
     if (h.t != -1.0f || i < F.bounces) normal = tnormal<COUNT>(S, pos, c);
+#ifdef RM_TDBL_NORMAL
+    if (!COUNT && (h.t != -1.0f || i < F.bounces)) {
+      const f3 n2 = tnormal<COUNT>(S, topaque(pos), c);
+      normal = mk(fminf(normal.x, n2.x), fminf(normal.y, n2.y), fminf(normal.z, n2.z));
+    }
+#endif
     if (h.t == -1.0f) {
       h.color = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
     } else {
@@ -651,7 +676,10 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
       h.color = point_light(F, h.color, normal, pos);
     }
     if (h.id == 7 && i < 3) {  // prevObject.material != MATTE here
-      const float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+#ifdef RM_TDBL_SHADOW
+      if (!COUNT) sh = fminf(sh, tshadow<COUNT, KL>(F, S, topaque(add(pos, muls(normal, 0.02f))), sub(lpos, pos), c));
+#endif
       color = muls(color, sh / (float)i);
     }
     color = add(color, divs(mul(h.color, prevColor), (float)i));
@@ -665,15 +693,30 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
 template <bool COUNT, int KL>
 __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
-  const THit h = tmarch<COUNT, KL>(S, ro, rd, false, c, F.prepv);
+  THit h = tmarch<COUNT, KL>(S, ro, rd, false, c, F.prepv);
+#ifdef RM_TDBL_MARCH
+  if (!COUNT) {
+    const THit h2 = tmarch<COUNT, KL>(S, topaque(ro), rd, false, c, F.prepv);
+    h.t = (h2.t == h.t) ? h.t : __builtin_nanf("");
+  }
+#endif
   if (h.t != -1.0f) {
     const f3 pos = add(ro, muls(rd, h.t));
-    const f3 normal = tnormal<COUNT>(S, pos, c, true, h.d);
+    f3 normal = tnormal<COUNT>(S, pos, c, true, h.d);
+#ifdef RM_TDBL_NORMAL
+    if (!COUNT) {
+      const f3 n2 = tnormal<COUNT>(S, topaque(pos), c, true, h.d);
+      normal = mk(fminf(normal.x, n2.x), fminf(normal.y, n2.y), fminf(normal.z, n2.z));
+    }
+#endif
     if (COUNT) c.lights++;
     color = point_light(F, h.color, normal, pos);
     if (h.id == 7) {
       const f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
-      const float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+#ifdef RM_TDBL_SHADOW
+      if (!COUNT) sh = fminf(sh, tshadow<COUNT, KL>(F, S, topaque(add(pos, muls(normal, 0.02f))), sub(lpos, pos), c));
+#endif
       return gamma(muls(color, sh));
     }
     if (F.bounces > 0) color = tbounce<COUNT, KL>(F, S, rd, pos, normal, color, h, c);
