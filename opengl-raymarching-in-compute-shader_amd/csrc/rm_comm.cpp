@@ -68,8 +68,11 @@ ncclConfig_t nonblocking_config() {
 }
 
 void poll_pause(int spins) {
-  if (spins < 64) std::this_thread::yield();
-  else std::this_thread::sleep_for(std::chrono::microseconds(spins < 256 ? 50 : 1000));
+  // Yield (a few us per poll) for the first ~10-40 ms: a frame or a bench's timed
+  // steps at N = 8 end within that, and a sleeping poll would add up to its
+  // period to the measured time.  Then back off: 100 us, and 1 ms past ~1 s.
+  if (spins < 20000) std::this_thread::yield();
+  else std::this_thread::sleep_for(std::chrono::microseconds(spins < 30000 ? 100 : 1000));
 }
 
 ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long timeout_ms) {

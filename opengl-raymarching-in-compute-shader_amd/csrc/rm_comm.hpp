@@ -45,7 +45,8 @@ ncclConfig_t nonblocking_config();
 // passed first (timeout_ms <= 0: no deadline).
 ncclResult_t wait_ready(const Rccl* r, const ncclComm_t* comms, int n, long timeout_ms);
 
-// Back-off for host polling loops: yields first, then sleeps up to 1 ms.
+// Back-off for host polling loops: yields for the first ~10-40 ms (no added
+// latency at the end of a short wait), then sleeps 100 us, then 1 ms.
 void poll_pause(int spins);
 
 // Tears down comms[0..n) of one process (the devices of a multi-GPU context, or
