@@ -17,6 +17,10 @@ shadows, 4x supersampling, 1 MI355X.
 Step k of K renders sweep frame floor(k * 120 / K): every run samples the whole
 sweep evenly, so `value` is the sweep mean.
 
+Timing: barrier + device synchronise, t0, the K steps, each rank's streams drained
++ device synchronise, t1, barrier; `value` uses the max over ranks of t1 - t0 (the
+host barrier's own round trip is outside the interval, the slowest rank's end is in).
+
 Rank 0 prints ONE JSON line.  Extra objects:
   roofline        : FP32-VALU issue roofline of the dominant kernel (k_sample /
                     k_pixel): achieved = SQ_INSTS_VALU per launch (committed
@@ -368,8 +372,15 @@ def main() -> int:
     for f in frames_timed:
         step(f)
     t_issue = time.perf_counter()
-    barrier()
+    # the end of the K steps on this rank: every librm stream drained (bounded on a
+    # communicator context) and the device synchronised; then the host barrier,
+    # whose own latency (a gloo round trip, ~0.1-1 ms) is not frame work.  The max
+    # over ranks below takes the slowest rank's end.
+    for rj in rs:
+        rj.synchronize()
+    torch.cuda.synchronize()
     t1 = time.perf_counter()
+    barrier()
     kernel_ms, launches = 0.0, 0
     for rj in rs:
         ms_j, n_j = rj.kernel_time_ms(reset=True)
