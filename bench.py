@@ -80,6 +80,12 @@ def bench_frames(steps: int) -> list:
 OPS = dict(march=116, reflect=116, shadow=117, normal=446, light=90, ray=33)
 VALU_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md), FMA = 2 ops
 VALU_LANE_PEAK_T = VALU_PEAK_TFLOPS / 2  # VALU lane-instructions/s
+# VALU issue slots: each SIMD issues one VALU slot per quad-cycle (4 cycles), in
+# which either one instruction issues, or two dual-issuable ones of different
+# waves (f32 add / mul / fma / mov with VGPR, literal or inline operands); an
+# SGPR operand, compares, selects, min / max take a whole slot, transcendentals
+# two (measured: tools/valu_peak.hip, profiles/r03_valu_peak.txt).
+VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 4  # G quad-cycle slots/s: 256 CUs x 4 SIMDs at 2.4 GHz
 HBM_PEAK_GBS = 8000.0      # HBM3E spec
 
 
@@ -462,6 +468,11 @@ def main() -> int:
     # lane-instructions/s.  frac = SQ_INSTS_VALU x 64 / kernel time / 78.65 T.
     valu_insts = pmc.get("SQ_INSTS_VALU") if pmc else None
     valu_issue = (valu_insts * 64 / (mean_kernel_ms * 1e-3) / 1e12) if valu_insts else None
+    # The same kernel against the SIMDs' VALU issue slots: its busy slots per launch
+    # (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2, committed PMC pass) per second of
+    # the kernel time measured here, over 614.4 G slots/s.
+    busy_quads = pmc.get("valu_busy_quads") if pmc else None
+    issue_rate = (busy_quads / (mean_kernel_ms * 1e-3) / 1e9) if busy_quads else None
     # The reference's brute-force work (SURVEY 8(d) op weights x the exact counters of
     # the frames timed): the kernel skips most of it by proof, so this rate is not
     # hardware utilisation and can exceed the peak.
@@ -532,7 +543,18 @@ def main() -> int:
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
                          "kernel_time_basis": kernel_time_basis,
                          "hbm_write_GBs": round(hbm_gbs, 2),
-                         "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6)},
+                         "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6),
+                         "issue": {"achieved": round(issue_rate, 2) if issue_rate else None,
+                                   "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU issue slots/s (quad-cycles)",
+                                   "frac": round(issue_rate / VALU_ISSUE_PEAK_G, 4) if issue_rate else None,
+                                   "busy_slots_per_launch": busy_quads,
+                                   "dual_issued_slots_per_launch": pmc.get("SQ_ACTIVE_INST_VALU2") if pmc else None,
+                                   "note": "frac above counts executed VALU lane-instructions at the FP32 "
+                                           "vector peak (157.3 TFLOP/s = every instruction dual-issued); "
+                                           "this one counts the SIMDs' VALU issue slots the kernel keeps "
+                                           "busy (a slot issues one instruction, or two dual-issuable "
+                                           "ones; streams that saturate it reach 0.92-0.96, "
+                                           "tools/valu_peak.hip)"}},
             "algorithmic_rate": {"ops_per_launch": int(ops_total / max(launches, 1)),
                                  "TFLOPs": round(achieved_tflops, 3),
                                  "vs_fp32_peak": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),

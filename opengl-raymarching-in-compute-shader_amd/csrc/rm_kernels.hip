@@ -56,6 +56,10 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   const bool prep = !reflected && F.prepv[PREP_VALID] != 0.0f;
   const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
   const float s0 = prep ? F.prepv[PREP_SLACK] : ray_s0(ro);
+  // ro in VGPRs: a primary ray's ro is the camera, uniform, and an SGPR operand
+  // keeps an f32 add / mul from dual issue (4 instead of 2 cycles per wave64
+  // instruction on gfx950, tools/valu_peak.hip), once per march step here.
+  ro = opaque(ro);
   LazyCull lc;
   lazy_init(lc, rd, rdl, s0, s1);
   // the provable-miss threshold mx (rm_scene.hpp "early exits"), formed where it

@@ -482,16 +482,20 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
   RM_STAT(8);
   if (__any(t >= lc.temin)) {
     const float plane = m;
-    float mp = __builtin_huge_valf();  // minimum over the evaluated primitives
     int idp = 7;
 
     RM_STAT(9);
     const float slack = __builtin_fmaf(lc.s1, t, lc.s0);
     const float inv2v = lc.inv2v, invp = lc.invp;
     const float pl = m + slack;  // plane(p_i) + slack
+    // The opU id among the evaluated primitives, later wins ties, compared with
+    // the running minimum m (plane included) rather than a separate minimum over
+    // the primitives: a primitive above the plane is never taken, which only
+    // matters when the plane wins (m == plane below: id 7); otherwise the winner
+    // v* < plane is <= every m before it and every later tie is taken, as with a
+    // primitives-only minimum.  One v_min per evaluation fewer (round 3).
     auto take = [&](float v, int k) {
-      idp = (v <= mp) ? k : idp;
-      mp = vmin(mp, v);
+      idp = (v <= m) ? k : idp;
       m = vmin(m, v);
     };
     // re-test k; returns true when k must be evaluated exactly at this step
@@ -506,9 +510,13 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       // (rounding is monotone); the fmas round once instead of twice, inside the
       // budgets' 2^-10 margin.
       const float tn = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), t);
-      const bool expired = t >= te;
+      // Evaluate exactly when the new expiry does not pass t: a lane whose te
+      // had not expired keeps te > t; an expired lane gets te = t exactly when
+      // g <= 0 (both budgets <= 0, as plane >= m), and also when g > 0 is too
+      // small to move t -- an extra exact evaluation, never a wrong skip.  One
+      // compare instead of two (round 3).
       te = te_max(te, tn);
-      return expired & !(g > 0.0f);
+      return te <= t;
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
@@ -548,7 +556,7 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       }
     }
     lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
-    lc.idb = (plane <= mp) ? 7 : idp;
+    lc.idb = (m == plane) ? 7 : idp;  // no primitive strictly below the plane
     lc.tb = t;
   }
   return m;

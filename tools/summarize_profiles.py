@@ -29,7 +29,7 @@ def main(src, tag, workload="cfg3", dst="profiles"):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, f"{tag}_kernel_stats.csv"))
     out = {}
-    for sub in ("fetch", "write", "sq", "sq2"):
+    for sub in ("fetch", "write", "sq", "sq2", "sq3"):
         p = os.path.join(src, sub)
         if not os.path.isdir(p):
             continue
@@ -46,6 +46,15 @@ def main(src, tag, workload="cfg3", dst="profiles"):
             cs["hbm_read_bytes_corrected"] = 2 * f
             cs["hbm_write_bytes"] = w
             cs["hbm_bytes_per_launch"] = 2 * f + w
+        # VALU issue (gfx950, tools/valu_peak.hip): a SIMD issues one VALU slot per
+        # quad-cycle, or two dual-issuable instructions of different waves in one;
+        # SQ_ACTIVE_INST_VALU counts each wave's issue quad-cycles (2 for a
+        # transcendental), SQ_ACTIVE_INST_VALU2 the quad-cycles that issued two.
+        if "SQ_ACTIVE_INST_VALU2" in cs and "SQ_ACTIVE_INST_VALU" in cs:
+            cs["valu_busy_quads"] = cs["SQ_ACTIVE_INST_VALU"] - cs["SQ_ACTIVE_INST_VALU2"]
+            if "GRBM_GUI_ACTIVE" in cs:  # summed over the 8 XCDs
+                cap = cs["GRBM_GUI_ACTIVE"] / 8 / 4 * 1024
+                cs["valu_issue_frac_same_run"] = cs["valu_busy_quads"] / cap
     # bench.py matches a summary to its workload through _meta
     kind, cfg, steps = (os.environ.get("PROF_KIND", "pixel"), os.environ.get("PROF_CFG", "3"),
                         os.environ.get("PROF_STEPS", "20"))
