@@ -58,13 +58,6 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-// max of two lazy-culling expiries (LazyCull::te): each is -inf or >= +0 (never
-// NaN: t >= 0 and the budgets are max'ed with t), a set on which the signed
-// integer order of the bit patterns is the float order -- one v_max_i32,
-// without the NaN-quieting canonicalisation LLVM puts around fmaxf of a phi.
-__device__ __forceinline__ float te_max(float a, float b) {
-  return __int_as_float(max(__float_as_int(a), __float_as_int(b)));
-}
 // GLSL min/max (y < x ? y : x) — used where a signed zero or NaN could differ.
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
@@ -138,6 +131,20 @@ constexpr float R_BLEND_LO = 4.63682f;   // >= |(3,2.5,2.5)| = 4.636809, box cir
 constexpr float R_TORUS = 3.0f;          // 2.5 + 0.5
 constexpr float R_CAPSULE = 3.45115f;    // >= |b-a|/2 + 1 = sqrt(24.03)/2 + 1 = 3.451050
 constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;  // segment midpoint
+
+// The cull test LB_k <= U of the torus and the capsule without the square root
+// (round 3: a v_sqrt takes two VALU issue slots): evaluate iff
+//   RN(x (1 - 2^-11)) <= RN(a^2),  a = RN(U + CULL_ABS + R),  x = |p - c|^2.
+// For a >= 0 this is sqrt(x) (1 - 2^-11)^(1/2) <= a up to 4 ulp, and
+// (1 - 2^-11)^(1/2) < CULL_REL_LO: the relative margin the v_sqrt form keeps
+// (2^-12, against a v_sqrt within 1.5 ulp) is kept, less 4 ulp.  For a < 0 the
+// v_sqrt form culls (LB >= -CULL_ABS - R > U); this one culls or evaluates, and
+// an extra exact evaluation is never wrong.  A NaN U culls in both.
+constexpr float CULL_SQ_LO = 1.0f - 0x1p-11f;
+__device__ __forceinline__ bool ball_needs(float x, float U, float R) {
+  const float a = U + (CULL_ABS + R);
+  return x * CULL_SQ_LO <= a * a;
+}
 
 #ifdef RM_STATS
 // Diagnostic build only: g_stats[k] counts waves reaching point k, g_stats[32+k]
@@ -260,8 +267,7 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   const float xtc = (o.cx2 + o.ay2) + tz * tz;
   const float xk = (kx * kx + ky * ky) + kz * kz;
   const float r0 = __builtin_amdgcn_sqrtf(x0), r1 = __builtin_amdgcn_sqrtf(x1);
-  const float rs = __builtin_amdgcn_sqrtf(xs), rt = __builtin_amdgcn_sqrtf(xtc);
-  const float rk = __builtin_amdgcn_sqrtf(xk);
+  const float rs = __builtin_amdgcn_sqrtf(xs);
   const float d7 = p.y + 5.5f;
   float U = vmin(d7, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
   U = vmin3(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f),
@@ -274,8 +280,8 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
     if (__builtin_fmaf(r1, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) d1 = sqrt_core(x1) - 3.0f;
     if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U)
       d4 = sd_blend(o, xs, blend, omblend);
-    if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) d5 = sd_torus(o, tz);
-    if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) d6 = sd_capsule(o, p);
+    if (ball_needs(xtc, U, R_TORUS)) d5 = sd_torus(o, tz);
+    if (ball_needs(xk, U, R_CAPSULE)) d6 = sd_capsule(o, p);
     float d = d0;
     id = 0;
     id = (d < d1) ? id : 1;
@@ -300,10 +306,10 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   if (__builtin_fmaf(rs, CULL_REL_LO, -(CULL_ABS + R_BLEND_LO)) <= U) {
     m = vmin(m, sd_blend(o, xs, blend, omblend));
   }
-  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {
+  if (ball_needs(xtc, U, R_TORUS)) {
     m = vmin(m, sd_torus(o, tz));
   }
-  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {
+  if (ball_needs(xk, U, R_CAPSULE)) {
     m = vmin(m, sd_capsule(o, p));
   }
   return m;
@@ -345,8 +351,8 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
   const float r0 = __builtin_amdgcn_sqrtf((o.ax * o.ax + o.ay2) + o.az2);
   const float r1 = __builtin_amdgcn_sqrtf((o.bx * o.bx + o.ay2) + o.az2);
   const float rs = __builtin_amdgcn_sqrtf((o.cx2 + o.ay2) + o.az2);
-  const float rt = __builtin_amdgcn_sqrtf((o.cx2 + o.ay2) + tz * tz);
-  const float rk = __builtin_amdgcn_sqrtf((kx * kx + ky * ky) + kz * kz);
+  const float xt = (o.cx2 + o.ay2) + tz * tz;
+  const float xk = (kx * kx + ky * ky) + kz * kz;
   const float e2 = 2.0f * (0.001f + 0x1p-22f * (((fabsf(pos.x) + fabsf(pos.y)) + fabsf(pos.z)) + 1.0f));
   float U = vmin(pos.y + 5.5f, __builtin_fmaf(r0, CULL_REL_HI, CULL_ABS - 3.0f));
   U = vmin3(U, __builtin_fmaf(r1, CULL_REL_HI, CULL_ABS - 3.0f),
@@ -371,13 +377,13 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
     my = vmin(my, ev_blend(py, blend, omblend));
     mz = vmin(mz, ev_blend(pz, blend, omblend));
   }
-  if (__builtin_fmaf(rt, CULL_REL_LO, -(CULL_ABS + R_TORUS)) <= U) {
+  if (ball_needs(xt, U, R_TORUS)) {
     if (!HAVE_C0) mc = vmin(mc, ev_torus(pos));
     mx = vmin(mx, ev_torus(px));
     my = vmin(my, ev_torus(py));
     mz = vmin(mz, ev_torus(pz));
   }
-  if (__builtin_fmaf(rk, CULL_REL_LO, -(CULL_ABS + R_CAPSULE)) <= U) {
+  if (ball_needs(xk, U, R_CAPSULE)) {
     if (!HAVE_C0) mc = vmin(mc, ev_capsule(pos));
     mx = vmin(mx, ev_capsule(px));
     my = vmin(my, ev_capsule(py));
@@ -504,18 +510,19 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       const float g = lb - m - slack;
-      // g <= 0 makes both budgets <= 0 (plane >= m), so max(.., t) is the
-      // "no budget" case; an expired te is <= t, so max(te, .) serves both the
-      // expired lane and the idle one.  t + max(b1, b2, 0) == max(t + b1, t + b2, t)
-      // (rounding is monotone); the fmas round once instead of twice, inside the
-      // budgets' 2^-10 margin.
-      const float tn = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), t);
-      // Evaluate exactly when the new expiry does not pass t: a lane whose te
-      // had not expired keeps te > t; an expired lane gets te = t exactly when
-      // g <= 0 (both budgets <= 0, as plane >= m), and also when g > 0 is too
-      // small to move t -- an extra exact evaluation, never a wrong skip.  One
-      // compare instead of two (round 3).
-      te = te_max(te, tn);
+      // The new expiry is the latest of the old one and the two budgets' ends;
+      // both budgets and the old expiry are valid, so their max is.  g <= 0 makes
+      // both budgets end at or before t (plane >= m), leaving an expired lane
+      // with te <= t: evaluated now and re-tested at its next step, whatever the
+      // exact value below t.  An idle lane keeps its te > t.  The fmas round once
+      // instead of twice (t + g b rather than t + RN(g b)), inside the budgets'
+      // 2^-10 margin.  One v_max3 (the float max: a te below t may be negative)
+      // replaces max3(b1, b2, t) followed by max(te, .) (round 3: one issue slot).
+      te = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), te);
+      // Evaluate exactly when the new expiry does not pass t: an expired lane
+      // whose budgets are <= 0, and also one whose tiny g > 0 cannot move t --
+      // an extra exact evaluation, never a wrong skip.  One compare instead of
+      // two (`expired & !(g > 0)`, round 3).
       return te <= t;
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);

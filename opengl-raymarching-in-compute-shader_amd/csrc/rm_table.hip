@@ -468,9 +468,14 @@ struct TLazy {
           const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
                                           1.0f - 0x1p-12f, -B[3]);
           const float g = lb - U - sl;
-          const bool expired = !(t < te(j));
-          te(j) = __builtin_fmaxf(te(j), __builtin_fmaxf(__builtin_fmaf(g, inv, t), t));
-          if (wany(expired && !(g > 0.0f))) wmask |= 1u << k;
+          // the later of the old expiry and the budget's end; an expired lane
+          // whose g <= 0 (or too small to move t) keeps te <= t and evaluates
+          // now, an idle lane keeps te > t; a NaN bound leaves te as it was and
+          // a NaN t evaluates (the negated compare).  One max and one compare
+          // fewer than max(te, max(t + g inv, t)) and `expired & !(g > 0)`
+          // (round 3, VALU issue slots: DESIGN.md §6).
+          te(j) = __builtin_fmaxf(te(j), __builtin_fmaf(g, inv, t));
+          if (wany(!(t < te(j)))) wmask |= 1u << k;
         }
       }
       temin = te(0);
@@ -481,6 +486,16 @@ struct TLazy {
     return dprev;
   }
 };
+
+// An opaque VGPR copy: a uniform value used as a VGPR operand (an f32 op with an
+// SGPR operand takes a whole VALU issue slot, with VGPRs two pair in one,
+// DESIGN.md §6), and the RM_TDBL_<PHASE> probes' opaque inputs (diagnostic
+// builds, tools/ab_kernel.py: a phase run twice, its marginal cost per frame).
+__device__ __forceinline__ float topaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ f3 topaque(f3 v) { return mk(topaque(v.x), topaque(v.y), topaque(v.z)); }
 
 struct THit {
   float t;  // -1: the dummy RayHit {-1, 0, -1, 1.0} (glsl:128)
@@ -494,6 +509,12 @@ struct THit {
 template <bool COUNT, int KL>
 __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c,
                                    const float* prep = nullptr) {
+  // ro in VGPRs (a primary ray's ro is the camera, uniform): every step's p(t)
+  // then pairs for dual issue instead of taking a whole slot per component, and
+  // the generic kernel spills less (28 -> 12 B of scratch per lane): -2.9 % per
+  // cfg3 frame (round 3).  The fast plane's parameters moved to
+  // VGPRs the same way measured +0.5 % against this (more spills).
+  ro = topaque(ro);
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   float t = 0.0f;
@@ -633,14 +654,6 @@ __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 
   }
   return res;
 }
-
-// Diagnostic builds only (RM_TDBL_<PHASE>, tools/ab_kernel.py): a phase run
-// twice on an opaque copy of its input, so its marginal cost shows per frame.
-__device__ __forceinline__ float topaque(float x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-__device__ __forceinline__ f3 topaque(f3 v) { return mk(topaque(v.x), topaque(v.y), topaque(v.z)); }
 
 // bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
 // the colour unchanged (glsl:181, 189-190): the loop stops there.
