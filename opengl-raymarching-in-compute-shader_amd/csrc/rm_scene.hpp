@@ -256,7 +256,7 @@ __device__ __forceinline__ float scene_exact(f3 p, float blend, float omblend, i
 //   U candidates: plane (exact), spheres |p-c| - 3, blend |p-c| - 2.5 (box inradius).
 // LB_k > U  =>  primitive k is strictly farther than the minimum: skip it.  The
 // branch for k runs when any lane of the wave needs it.
-template <bool WANT_ID>
+template <bool WANT_ID, bool PLANE_U = false>
 __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, int& id) {
   const Offs o = offsets(p);
   const float tz = p.z - 10.0f;
@@ -297,6 +297,18 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
     return d;
   }
   float m = d7;  // running minimum over the plane and the evaluated primitives
+#ifdef RM_SHADOW_PU
+  if (PLANE_U) {
+    // U = the plane alone, every cull test squared (no v_sqrt): the shadow
+    // march starts 0.02 above the floor, where the plane is the tightest bound
+    if (ball_needs(x0, d7, 3.0f)) m = vmin(m, sqrt_core(x0) - 3.0f);
+    if (ball_needs(x1, d7, 3.0f)) m = vmin(m, sqrt_core(x1) - 3.0f);
+    if (ball_needs(xs, d7, R_BLEND_LO)) m = vmin(m, sd_blend(o, xs, blend, omblend));
+    if (ball_needs(xtc, d7, R_TORUS)) m = vmin(m, sd_torus(o, tz));
+    if (ball_needs(xk, d7, R_CAPSULE)) m = vmin(m, sd_capsule(o, p));
+    return m;
+  }
+#endif
   if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
     m = vmin(m, sqrt_core(x0) - 3.0f);
   }
