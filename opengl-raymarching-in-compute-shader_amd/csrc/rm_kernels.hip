@@ -283,27 +283,16 @@ __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, C
   int dummy;
   RM_STAT(29);
   const float ex = shadow_exit_init(F.k, ro, rd);
-#ifdef RM_SHADOW_KV
-  const float kv = opaque(F.k);
-#endif
   for (int i = 0; i < 16; ++i) {
     if (lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;
       return res;
     }
-#ifdef RM_SHADOW_PU
     float h = scene_cull<false, true>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
-#else
-    float h = scene_cull<false>(add(ro, muls(rd, t)), F.blend, F.omblend, dummy);
-#endif
     RM_STAT(2);
     if (COUNT) c.shadow++;
     if (h < 0.001f) return 0.05f;
-#ifdef RM_SHADOW_KV
-    res = shadow_min(res, kv, h, t);
-#else
     res = shadow_min(res, F.k, h, t);
-#endif
     t += h;
   }
   return res;

@@ -297,10 +297,12 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
     return d;
   }
   float m = d7;  // running minimum over the plane and the evaluated primitives
-#ifdef RM_SHADOW_PU
   if (PLANE_U) {
-    // U = the plane alone, every cull test squared (no v_sqrt): the shadow
-    // march starts 0.02 above the floor, where the plane is the tightest bound
+    // U = the plane alone and every cull test squared (ball_needs): no v_sqrt at
+    // all.  The shadow march starts 0.02 above the floor, where the plane is the
+    // tightest bound anyway; the spheres' bounds in U cost three transcendentals
+    // per step for the few steps they tighten (round 3: -1.3 % per cfg3 frame,
+    // DESIGN.md §4.4 item 13 f).
     if (ball_needs(x0, d7, 3.0f)) m = vmin(m, sqrt_core(x0) - 3.0f);
     if (ball_needs(x1, d7, 3.0f)) m = vmin(m, sqrt_core(x1) - 3.0f);
     if (ball_needs(xs, d7, R_BLEND_LO)) m = vmin(m, sd_blend(o, xs, blend, omblend));
@@ -308,7 +310,6 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
     if (ball_needs(xk, d7, R_CAPSULE)) m = vmin(m, sd_capsule(o, p));
     return m;
   }
-#endif
   if (__builtin_fmaf(r0, CULL_REL_LO, -(CULL_ABS + 3.0f)) <= U) {
     m = vmin(m, sqrt_core(x0) - 3.0f);
   }
