@@ -135,9 +135,10 @@ constexpr float CAP_MX = -4.05f, CAP_MY = 0.05f, CAP_MZ = -29.05f;  // segment m
 // The cull test LB_k <= U of the torus and the capsule without the square root
 // (round 3: a v_sqrt takes two VALU issue slots): evaluate iff
 //   RN(x (1 - 2^-11)) <= RN(a^2),  a = RN(U + CULL_ABS + R),  x = |p - c|^2.
-// For a >= 0 this is sqrt(x) (1 - 2^-11)^(1/2) <= a up to 4 ulp, and
-// (1 - 2^-11)^(1/2) < CULL_REL_LO: the relative margin the v_sqrt form keeps
-// (2^-12, against a v_sqrt within 1.5 ulp) is kept, less 4 ulp.  For a < 0 the
+// For a >= 0 this is sqrt(x) (1 - 2^-11)^(1/2) <= a up to the roundings, and
+// (1 - 2^-11)^(1/2) < CULL_REL_LO: a cull keeps the 2^-12 relative margin of the
+// v_sqrt form less at most 0.5 ulp of a (the v_sqrt form: up to 1.5 ulp;
+// tests/test_cull_bounds.py checks this on samples at the boundary).  For a < 0 the
 // v_sqrt form culls (LB >= -CULL_ABS - R > U); this one culls or evaluates, and
 // an extra exact evaluation is never wrong.  A NaN U culls in both.
 constexpr float CULL_SQ_LO = 1.0f - 0x1p-11f;
