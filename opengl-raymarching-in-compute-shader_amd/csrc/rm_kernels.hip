@@ -98,7 +98,8 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll
     for (int k = 0; k < 5; ++k)
       lc.te[k] = vmax3(F.prepv[PREP_G + k] * lc.inv2v, F.prepv[PREP_H + k] * lc.invp, 0.0f);
-    lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
+    lc.tegrp = vmin(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[4]);
+    lc.temin = vmin(lc.tegrp, lc.te[3]);
     if (COUNT) c.march++;
     dl = d0;
     t = d0;

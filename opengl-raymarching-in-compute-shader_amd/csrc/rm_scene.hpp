@@ -430,6 +430,7 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
+  float tegrp;   // min over te[] but the torus's: one compare for four primitives
   float s0, s1;  // slack(t) = s0 + s1 t >= 2^-14 (|ro|_1 + |rd| t + 64)  (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
@@ -472,6 +473,7 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
 #pragma unroll
   for (int k = 0; k < 5; ++k) c.te[k] = NEG;
   c.temin = NEG;
+  c.tegrp = NEG;
   const float rdlen = rdl * (1.0f + 0x1p-16f);  // >= |rd|
   c.inv2v = (0.5f * (1.0f - 0x1p-10f)) * __builtin_amdgcn_rcpf(rdlen) * (1.0f - 0x1p-16f);
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
@@ -541,21 +543,27 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
-    if (__any(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
+    // One wave vote for the four primitives other than the torus, which takes
+    // half of the re-tests (cfg3 frame 60: 10 of 21 per wave): a block entered
+    // for the torus alone then costs one compare instead of four (round 3,
+    // VALU issue slots: -1.0 % cfg3, -2.0 % cfg2 per frame).  Evaluation order,
+    // hence opU's tie rule, is unchanged.
+    const bool GRP = __any(t >= lc.tegrp);
+    if (GRP && __any(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
       if (retest(x0, 3.0f, lc.te[0], 0)) {
         RM_STAT(10);
         take(sqrt_core(x0) - 3.0f, 0);
       }
     }
-    if (__any(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
+    if (GRP && __any(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
       if (retest(x1, 3.0f, lc.te[1], 1)) {
         RM_STAT(11);
         take(sqrt_core(x1) - 3.0f, 1);
       }
     }
-    if (__any(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
+    if (GRP && __any(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
       if (retest(xs, R_BLEND_LO, lc.te[2], 2)) {
         RM_STAT(12);
@@ -569,14 +577,15 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
         take(sd_torus(o, tz), 5);
       }
     }
-    if (__any(t >= lc.te[4])) {  // capsule, glsl:120
+    if (GRP && __any(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
       if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4)) {
         RM_STAT(14);
         take(sd_capsule(o, p), 6);
       }
     }
-    lc.temin = vmin3(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[3], lc.te[4]);
+    lc.tegrp = vmin(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[4]);
+    lc.temin = vmin(lc.tegrp, lc.te[3]);
     lc.idb = (m == plane) ? 7 : idp;  // no primitive strictly below the plane
     lc.tb = t;
   }
