@@ -41,18 +41,20 @@ $(PKG)/build/%.o: $(CSRC)/%.hip $(RM_HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # rm_kernels.hip is built twice: k_pixel + k_unshard (rm_kernels.o),
-# and k_sample alone without SLP vectorisation (rm_kernels_aa.o): pairing its f32
-# adds / muls into packed v_pk_* ops costs register moves to form the pairs and
-# measured 3.9 % slower per cfg3 frame; k_pixel keeps SLP.  Both at -O2, which
-# measured 0.4-2 % faster than -O3 for each (round 3, profiles/r03_compiler_ab.txt).
-KFLAGS   := $(HIPFLAGS) -O2
+# and k_sample alone (rm_kernels_aa.o), both without SLP vectorisation: pairing
+# f32 adds / muls into packed v_pk_* ops costs register moves to form the pairs
+# (k_sample: 3.9 % slower per cfg3 frame), and since round 3's issue-slot changes
+# it makes k_pixel spill 9 VGPRs (32 B of scratch per lane; none without SLP,
+# round 4).  Both at -O2, which measured 0.4-2 % faster than -O3 for each (round
+# 3, profiles/r03_compiler_ab.txt).
+KFLAGS   := $(HIPFLAGS) -O2 -fno-slp-vectorize
 $(PKG)/build/rm_kernels.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(KFLAGS) -DRM_KERNELS_PIXEL_ONLY -c $< -o $@
 
 $(PKG)/build/rm_kernels_aa.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(KFLAGS) -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c $< -o $@
+	$(HIPCC) $(KFLAGS) -DRM_KERNELS_AA_ONLY -c $< -o $@
 
 # the scene-table kernels without SLP vectorisation too (generic -2.7 %, the
 # hiprtc-specialised ones get the same flag in rm_jit.hip: -6.5 % per cfg3 frame)

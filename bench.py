@@ -202,6 +202,74 @@ def comm_ids(n: int, rank: int) -> list:
     return ids
 
 
+def default_batch(config: int, dist_on: bool, one_comm: bool) -> int:
+    """Frames per launch when --batch is not given (measured).
+
+    One GPU: cfg1 / cfg2 frames (4K / 32K one-wave workgroups) are shorter than their
+    longest waves and cannot fill 256 CUs alone; 10 frames per launch on 2 contexts
+    render at 0.0146 / 0.0653 ms per frame against 0.0593 / 0.0906 with 3 frames in
+    flight (round 4, tools/probe_batch.py).  The 4K / 8K supersampled frames fill the
+    chip by themselves; 3 frames in flight and batches measure the same there."""
+    if one_comm:
+        return 4  # N > 1, one communicator: gather batch j while batch j + 1 renders
+    if dist_on:
+        return 1
+    return 10 if config in (1, 2) else 1
+
+
+def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
+    """Per-rank render / gather / assembly split (rm_frame_phases: HIP events around the
+    render kernel, the ncclGather and rank 0's assembly) over EVERY timed frame, re-rendered
+    eagerly after the timed region (one frame, or one batch, at a time), so a scaling
+    shortfall can be attributed to render imbalance or to the gather."""
+    import torch.distributed as dist
+    vals = {"render_ms": [], "gather_ms": [], "assemble_ms": []}
+    r.enable_timing(True)
+    for i in range(0, len(frames), batch):
+        chunk = frames[i:i + batch]
+        if batch > 1:
+            r.dispatch_frames([uniforms(f) for f in chunk])
+        else:
+            r.dispatch(uniforms(chunk[0]))
+        ph = r.frame_phases()  # synchronizes
+        for k in vals:
+            vals[k].append(ph[k] / len(chunk))
+    r.enable_timing(False)
+    r.kernel_time_ms(reset=True)
+    mine = {"rank": rank}
+    for k, v in vals.items():
+        mine[k.replace("_ms", "_mean_ms")] = round(float(np.mean(v)), 4)
+        mine[k.replace("_ms", "_max_ms")] = round(float(np.max(v)), 4)
+    allp = [None] * ws
+    dist.all_gather_object(allp, mine)
+    return {"per_rank": allp,
+            "frames": len(frames), "frames_per_sample": batch,
+            "max_render_mean_ms": max(p["render_mean_ms"] for p in allp),
+            "max_render_max_ms": max(p["render_max_ms"] for p in allp),
+            "max_gather_mean_ms": max(p["gather_mean_ms"] for p in allp),
+            "max_gather_max_ms": max(p["gather_max_ms"] for p in allp),
+            "assemble_mean_ms": allp[0]["assemble_mean_ms"],
+            "note": "every timed frame re-rendered eagerly after the timed region, one "
+                    + ("frame" if batch == 1 else f"batch of {batch} frames (values per frame)")
+                    + " at a time; gather_ms runs from this rank's render end to its gather end, "
+                      "so it includes waiting for the slowest peer's shard"}
+
+
+def rccl_report(rs, rank, ws):
+    """What RCCL itself reports for every communicator of every rank (ncclCommCount,
+    ncclCommUserRank, ncclCommCuDevice, ncclGetVersion via rm_comm_rccl_info): the line
+    proves how many ranks RCCL formed, not only torch's WORLD_SIZE."""
+    import torch.distributed as dist
+    mine = {"rank": rank, "comms": [rj.rccl_info() for rj in rs]}
+    allr = [None] * ws
+    dist.all_gather_object(allr, mine)
+    counts = sorted({c["count"] for p in allr for c in p["comms"]})
+    ok = all(c["count"] == ws and c["user_rank"] == p["rank"] for p in allr for c in p["comms"])
+    return {"version": allr[0]["comms"][0]["version"] if allr[0]["comms"] else None,
+            "nranks_seen": counts, "world_size": ws, "all_communicators_match": ok,
+            "per_rank": allr}
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -226,6 +294,16 @@ def main() -> int:
                          "last long waves leave idle (1 = one context, frames in turn; "
                          "0 = 3 on one GPU, 4 on a sharded frame, whose per-rank share is "
                          "shorter than its longest waves)")
+    ap.add_argument("--batch", type=int, default=-1,
+                    help="frames per launch (rm_dispatch_frames: one grid over B frames, so frame "
+                         "k+1's waves fill the SIMDs frame k's longest waves leave idle); 1 = one "
+                         "rm_dispatch per frame; -1 = the measured default for the configuration")
+    ap.add_argument("--comms", type=int, default=0,
+                    help="N > 1: communicators per rank.  0 = one per in-flight context (frames in "
+                         "flight on separate streams, each gathering behind its own render); 1 = one "
+                         "context and one communicator per rank: batches of --batch frames render in "
+                         "one launch and move in one ncclGather on the context's gather stream, "
+                         "ordered by events, while the next batch renders")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="N > 1: gather frame f on a second stream while frame f+1 renders "
                          "(double-buffered shard images); 0 = render, gather, assemble in turn")
@@ -279,8 +357,14 @@ def main() -> int:
     # Frames in flight: consecutive frames go to separate contexts, each with its own
     # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
     # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
-    nfl = args.inflight if args.inflight > 0 else (3 if not dist_on else 4)
+    one_comm = dist_on and args.comms == 1
+    batch = args.batch if args.batch > 0 else default_batch(args.config, dist_on, one_comm)
+    batch = max(1, min(batch, rm.RM_MAX_BATCH, args.steps))
+    # contexts in flight: 3 frames on one GPU, 2 batches, 4 frames of a sharded step
+    nfl = args.inflight if args.inflight > 0 else ((2 if batch > 1 else 3) if not dist_on else 4)
     nfl = nfl if (not dist_on or args.pipeline) else 1
+    if one_comm:
+        nfl = 1  # one context, one communicator; batches overlap through its gather stream
 
     ucache = {}
 
@@ -331,6 +415,23 @@ def main() -> int:
         nstep[0] += 1
         render(j, f)
 
+    barr = {}  # rm_uniforms arrays of the batches, built before the timed region
+
+    def issue(frames):
+        # the frames of a run of steps: one rm_dispatch per frame, or rm_dispatch_frames
+        # per `batch` consecutive frames (the contexts take the batches in turn)
+        if batch <= 1 or use_graph:
+            for f in frames:
+                step(f)
+            return
+        for i in range(0, len(frames), batch):
+            key = tuple(frames[i:i + batch])
+            if key not in barr:
+                barr[key] = [uniforms(f) for f in key]
+            j = nstep[0] % nfl
+            nstep[0] += 1
+            rs[j].dispatch_frames(barr[key])
+
     def barrier():
         # librm's own wait first: on a communicator context it is bounded
         # (rm_comm_set_timeout) and turns a hung gather into RM_ERR_COMM
@@ -349,8 +450,11 @@ def main() -> int:
         s0, k = time.perf_counter(), 0
         while True:
             for _ in range(nfl):
-                step(frames_timed[k % args.steps])
-                k += 1
+                n = max(batch, 1) if not use_graph else 1
+                issue([frames_timed[(k + i) % args.steps] for i in range(n)])
+                k += n
+            for rj in rs:
+                rj.synchronize()
             torch.cuda.synchronize()
             more = (time.perf_counter() - s0) * 1e3 < args.spinup_ms
             if dist_on:
@@ -361,8 +465,7 @@ def main() -> int:
                 break
         nstep[0] = 0
     # ---- warmup (untimed): the first W frames of the same list ----
-    for k in range(args.warmup):
-        step(frames_timed[k % args.steps])
+    issue([frames_timed[k % args.steps] for k in range(args.warmup)])
     barrier()
 
     # ---- timed region: exactly K steps ----
@@ -370,13 +473,15 @@ def main() -> int:
     # below, so no per-launch timing events are recorded in the timed region)
     for f in frames_timed:
         uniforms(f)
+    for i in range(0, len(frames_timed), batch):
+        key = tuple(frames_timed[i:i + batch])
+        barr.setdefault(key, [uniforms(f) for f in key])
     for rj in rs:
         rj.enable_timing(nfl == 1)
         rj.kernel_time_ms(reset=True)
     barrier()
     t0 = time.perf_counter()
-    for f in frames_timed:
-        step(f)
+    issue(frames_timed)
     t_issue = time.perf_counter()
     # the end of the K steps on this rank: every librm stream drained (bounded on a
     # communicator context) and the device synchronised; then the host barrier,
@@ -394,43 +499,43 @@ def main() -> int:
         launches += n_j
         rj.enable_timing(False)
     kernel_time_basis = "HIP events on the launch stream over the timed region"
-    if nfl > 1 or (use_graph and dist_on):
+    batched = batch > 1 and not use_graph
+    mean_launch_ms = None
+    if nfl > 1 or batch > 1 or (use_graph and dist_on):
         # Overlapping frames stretch each launch's event interval (and on a
         # communicator context a graph launch holds the gather and the assembly
         # too), so the roofline takes its kernel time from the same frames rendered
         # one at a time on one context through rm_dispatch, whose HIP events
         # bracket the render kernel alone (untimed for `value`).
+        # A batched run re-renders the same batches one at a time: the events
+        # bracket each batch's launch, which counts its frames.
         barrier()
         r.enable_timing(True)
         r.kernel_time_ms(reset=True)
-        for f in frames_timed:
-            r.dispatch(uniforms(f))
+        nlaunch = 0
+        if batched:
+            for i in range(0, len(frames_timed), batch):
+                r.dispatch_frames(barr[tuple(frames_timed[i:i + batch])])
+                nlaunch += 1
+        else:
+            for f in frames_timed:
+                r.dispatch(uniforms(f))
+                nlaunch += 1
         barrier()
         kernel_ms, launches = r.kernel_time_ms(reset=True)
         r.enable_timing(False)
         kernel_time_basis = ("HIP events around the render kernel, the timed frames re-rendered "
-                             "one at a time through rm_dispatch (the timed region overlaps frames)")
+                             + (f"in their batches of {batch}, one launch at a time through "
+                                "rm_dispatch_frames" if batched else "one at a time through rm_dispatch")
+                             + " (the timed region overlaps frames)")
+        mean_launch_ms = kernel_ms / max(nlaunch, 1)
     elapsed = t1 - t0
     phases = None
+    rccl = None
     if dist_on:
-        # per-rank split of one untimed eager frame (rm_frame_phases: HIP events around
-        # the render kernel, the ncclGather and rank 0's assembly), so a scaling
-        # shortfall can be attributed to render imbalance or to the gather
-        r.enable_timing(True)
-        r.dispatch(uniforms(frames_timed[-1]))
-        mine = dict(rank=rank, **{k: round(v, 4) for k, v in r.frame_phases().items()})
-        r.enable_timing(False)
-        r.kernel_time_ms(reset=True)
-        allp = [None] * ws
-        dist.all_gather_object(allp, mine)
-        phases = {"per_rank": allp,
-                  "max_render_ms": max(p["render_ms"] for p in allp),
-                  "max_gather_ms": max(p["gather_ms"] for p in allp),
-                  "assemble_ms": allp[0]["assemble_ms"],
-                  "note": "one untimed frame (the last sweep frame) per rank; gather_ms runs from "
-                          "this rank's render end to its gather end, so it includes waiting for "
-                          "the slowest peer's shard"}
+        phases = frame_phase_stats(r, frames_timed, uniforms, batch if one_comm else 1, rank, ws)
         barrier()
+        rccl = rccl_report(rs, rank, ws)
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -456,9 +561,12 @@ def main() -> int:
             cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
     mean_kernel_ms = kernel_ms / max(launches, 1)
     kname = "k_sample" if cfg["aa"] else "k_pixel"
+    if batched and scene is None:
+        kname += "_frames"  # the batched kernels (grid.z = frame); PMC values per frame
     if scene is not None:
         kname = "k_table_sample" if cfg["aa"] else "k_table_pixel"
-    pmc, traffic_src = pmc_entry(kname + "<false>", f"cfg{args.config}" + ("-spec" if spec else ""))
+    pmc, traffic_src = pmc_entry(kname if kname.endswith("_frames") else kname + "<false>",
+                                 f"cfg{args.config}" + ("-spec" if spec else ""))
     traffic = int(pmc["hbm_bytes_per_launch"]) if pmc else None
     # Roofline of the dominant kernel: the FP32 VALU issue rate.  SQ_INSTS_VALU
     # (wave64 VALU instructions per launch, committed PMC pass over the bench's own
@@ -473,6 +581,8 @@ def main() -> int:
     # the kernel time measured here, over 614.4 G slots/s.
     busy_quads = pmc.get("valu_busy_quads") if pmc else None
     issue_rate = (busy_quads / (mean_kernel_ms * 1e-3) / 1e9) if busy_quads else None
+    # ... and per frame of the timed region's throughput (frames in flight / batched)
+    issue_tput = (busy_quads / (elapsed / frames) / 1e9) if busy_quads else None
     # The reference's brute-force work (SURVEY 8(d) op weights x the exact counters of
     # the frames timed): the kernel skips most of it by proof, so this rate is not
     # hardware utilisation and can exceed the peak.
@@ -526,7 +636,11 @@ def main() -> int:
                                    + (" (scene table, specialised)" if spec else ""), "width": W, "height": H,
                        "bounces": cfg["bounces"], "aa": cfg["aa"],
                        "shadow": "hard" if cfg["shadow"] == rm.RM_SHADOW_HARD else "soft",
-                       "kernel": kname, "hipgraph": bool(use_graph), "frames_in_flight": nfl,
+                       "kernel": kname, "hipgraph": bool(use_graph),
+                       "contexts_in_flight": nfl,
+                       "frames_per_launch": batch if batched else 1,
+                       "frames_in_flight": nfl * (batch if batched else 1),
+                       "communicators_per_rank": (1 if one_comm else nfl) if dist_on else 0,
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        + (" (pipelined)" if args.pipeline else "")
                                        if dist_on else "single GPU")},
@@ -541,6 +655,9 @@ def main() -> int:
                          "traffic": traffic, "traffic_source": traffic_src,
                          "valu_insts_per_launch": valu_insts, "pmc_frames": pmc_frames(traffic_src),
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
+                         "mean_launch_ms": round(mean_launch_ms, 4) if mean_launch_ms else None,
+                         "per": "frame" + (f" (launches of {batch} frames: PMC values, kernel time and "
+                                           "traffic divided by the frames of a launch)" if batched else ""),
                          "kernel_time_basis": kernel_time_basis,
                          "hbm_write_GBs": round(hbm_gbs, 2),
                          "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 6),
@@ -548,13 +665,16 @@ def main() -> int:
                                    "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU issue slots/s (quad-cycles)",
                                    "frac": round(issue_rate / VALU_ISSUE_PEAK_G, 4) if issue_rate else None,
                                    "busy_slots_per_launch": busy_quads,
+                                   "throughput_frac": (round(issue_tput / VALU_ISSUE_PEAK_G, 4)
+                                                       if issue_tput else None),
                                    "dual_issued_slots_per_launch": pmc.get("SQ_ACTIVE_INST_VALU2") if pmc else None,
                                    "note": "frac above counts executed VALU lane-instructions at the FP32 "
                                            "vector peak (157.3 TFLOP/s = every instruction dual-issued); "
                                            "this one counts the SIMDs' VALU issue slots the kernel keeps "
                                            "busy (a slot issues one instruction, or two dual-issuable "
                                            "ones; streams that saturate it reach 0.92-0.96, "
-                                           "tools/valu_peak.hip)"}},
+                                           "tools/valu_peak.hip); throughput_frac divides the same "
+                                           "busy slots per frame by ms_per_step instead"}},
             "algorithmic_rate": {"ops_per_launch": int(ops_total / max(launches, 1)),
                                  "TFLOPs": round(achieved_tflops, 3),
                                  "vs_fp32_peak": round(achieved_tflops / VALU_PEAK_TFLOPS, 4),
@@ -563,6 +683,7 @@ def main() -> int:
                                          "proof, so this is not a utilisation"},
             "work": cnt_total,
             "phases": phases,
+            "rccl": rccl,
             "cpu_baseline": cpu,
             "parity": parity,
         }

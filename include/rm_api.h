@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define RM_API_VERSION 3
+#define RM_API_VERSION 4
+#define RM_CONFIG_MAGIC 0x34434D52u /* "RMC4" little-endian: rm_config layout of API version 4 */
 
 /* ---- status codes --------------------------------------------------------- */
 #define RM_OK 0
@@ -107,10 +108,14 @@ typedef struct rm_counters {
 } rm_counters;
 
 typedef struct rm_config {
-  /* sizeof(rm_config) (API version 3; rm_config_init sets it).  A host built
-   * against an older header passes a smaller struct whose first word is the
-   * width: rm_create refuses it (RM_ERR_INVALID) instead of reading past it. */
+  /* sizeof(rm_config) and RM_CONFIG_MAGIC (rm_config_init sets both).  rm_create
+   * refuses a config where either differs (RM_ERR_INVALID) instead of reading
+   * a stale layout: a v1/v2 host's first two words are width and height, a v3
+   * host's second word is its width (<= 65536), and none of them can equal the
+   * magic, whatever the struct sizes happen to be (a v3 struct has
+   * the same size as this one on LP64). */
   uint32_t struct_size;
+  uint32_t magic;
   int32_t width;      /* image width  (SCREEN_WIDTH,  main.cpp:16) */
   int32_t height;     /* image height (SCREEN_HEIGHT, main.cpp:17) */
   int32_t device;     /* HIP device ordinal; -1 = current device */
@@ -175,6 +180,23 @@ int rm_default_uniforms(rm_uniforms *u);
 /* Render one frame with the current uniforms. Asynchronous on the context's
  * stream (== glDispatchCompute, main.cpp:123). */
 int rm_dispatch(rm_ctx *ctx);
+/* Render frames[0..n) (API version 4), n <= RM_MAX_BATCH: the same images as
+ * rm_set_uniforms(frames[k]) + rm_dispatch for k = 0..n-1, in one launch.  The
+ * frames of a batch render concurrently, so the waves of frame k+1 fill the
+ * SIMDs that frame k's longest waves leave idle (one tail per batch instead of
+ * one per frame).  Asynchronous on the context's stream.  Afterwards the
+ * context's uniforms are frames[n-1], its image (rm_read_rgba8 / _rgba32f,
+ * rm_get_output_rgba8) holds frame n-1, and rm_read_frame_rgba8 /
+ * rm_read_frame_rgba32f read any frame k of the batch (frames 0..n-2 live in a
+ * ring the context allocates, n-1 images of each enabled format).  On a
+ * communicator context (rm_comm_init, rm_config.ngpus) every rank renders its
+ * shards of the n frames in one launch, one ncclGather moves all n shards, and
+ * rank 0 assembles the n frames; the gather runs on a second stream of the
+ * context, so the next batch renders while this one gathers.  Frames with a
+ * different AA setting render in separate launches; a runtime scene table
+ * renders one launch per frame.  Not available with cfg.counters. */
+#define RM_MAX_BATCH 32
+int rm_dispatch_frames(rm_ctx *ctx, const rm_uniforms *frames, int32_t n);
 /* Wait for all work queued on the context (== glMemoryBarrier + the
  * implicit sync of the draw, main.cpp:125-134).  On a context with a
  * communicator this wait (and the one inside every readback) is a bounded
@@ -187,6 +209,10 @@ int rm_synchronize(rm_ctx *ctx);
  * packed [rows_cap][width] shard image is read (flip_y must be 0). */
 int rm_read_rgba8(rm_ctx *ctx, uint8_t *dst, size_t row_pitch, int flip_y);
 int rm_read_rgba32f(rm_ctx *ctx, float *dst, size_t row_pitch, int flip_y);
+/* Frame k of the last rm_dispatch_frames batch (k = n-1 is the context's image;
+ * after a plain rm_dispatch only k = 0 exists).  Same layout rules as above. */
+int rm_read_frame_rgba8(rm_ctx *ctx, int32_t k, uint8_t *dst, size_t row_pitch, int flip_y);
+int rm_read_frame_rgba32f(rm_ctx *ctx, int32_t k, float *dst, size_t row_pitch, int flip_y);
 /* Counters of the last dispatch (requires cfg.counters). */
 int rm_get_counters(rm_ctx *ctx, rm_counters *out);
 /* Per-pixel sdf() evaluation counts of the last dispatch, summed over the
@@ -331,6 +357,15 @@ int rm_comm_check(rm_ctx *ctx);
 /* The context's communicator: rank / size (0 / 1 without one), and the devices
  * a multi-GPU context drives (*ngpus = 1 for a one-GPU context). */
 int rm_comm_info(const rm_ctx *ctx, int32_t *rank, int32_t *nranks, int32_t *ngpus);
+/* What RCCL itself reports for the context's communicator (API version 4):
+ * ncclCommCount, ncclCommUserRank and ncclCommCuDevice of the communicator
+ * (device 0's for a multi-GPU context, whose every device is checked to be user
+ * rank i of ngpus on its own device) and ncclGetVersion.  RM_ERR_COMM when RCCL's
+ * view differs from the context's (rank, nranks, device).  Without a
+ * communicator: *count = 0, *user_rank = *hip_device = -1, *version = 0.  Any
+ * pointer may be NULL. */
+int rm_comm_rccl_info(rm_ctx *ctx, int32_t *count, int32_t *user_rank, int32_t *hip_device,
+                      int32_t *version);
 
 /* ---- row sharding helpers (pure functions) ------------------------------- */
 int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);

@@ -25,8 +25,10 @@ void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int nshards, int rows_cap, hipStream_t s);
+                          int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
+hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
 }  // namespace rm
+static_assert(RM_MAX_BATCH == rmd::kMaxBatch, "rm_api.h RM_MAX_BATCH == rm_scene.hpp kMaxBatch");
 
 // The graph path: the captured frame (the render kernel, and for a rank of an
 // RCCL-gathered frame the gather and the assembly after it) whose render node
@@ -62,6 +64,7 @@ struct rm_ctx {
   bool dispatched = false;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  std::vector<int> ev_frames;  // frames each timed launch rendered (a batch: n)
   size_t ev_used = 0;
   double total_ms = 0.0;
   int64_t launches = 0;
@@ -86,6 +89,26 @@ struct rm_ctx {
   // phase events of the last timed eager dispatch: render start / end, gather end, assembly end
   hipEvent_t ph[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ph_recorded = false, ph_comm = false;
+  // frame batches (rm_dispatch_frames)
+  int batch_n = 1;                  // frames of the last dispatch (a plain dispatch: 1)
+  std::vector<uint8_t*> ring8;      // frames 0..n-2 of the last batch (rank 0 of a communicator: assembled)
+  std::vector<float*> ring32;
+  // communicator contexts: two batch slots, so batch j + 1 renders while batch j
+  // gathers on gstream.  A slot's send8 / send32 hold this rank's shards of the
+  // batch's frames, [n][rows][width]; rank 0's is the whole gather buffer,
+  // [nranks][n][rows][width], its own shards rendering in place into [0].
+  struct BatchSlot {
+    uint8_t* send8 = nullptr;
+    float* send32 = nullptr;
+    int cap = 0;                   // frames the buffers hold
+    hipEvent_t rendered = nullptr; // the batch's render, on stream
+    hipEvent_t freed = nullptr;    // its gather and assembly, on gstream
+    bool pending = false;          // freed recorded and not yet waited for
+  } bslot[2];
+  int bnext = 0, blast = -1;        // the next slot; the slot of the last batch
+  hipStream_t gstream = nullptr;    // gathers + assembly of batches
+  hipEvent_t gdone = nullptr;       // the last batch's work on gstream
+  bool gdone_pending = false;       // plain dispatches order after it
   // a multi-GPU context (rm_config.ngpus): one shard context per device, subs[0] = rank 0
   std::vector<rm_ctx*> subs;
   std::string err;
@@ -226,7 +249,9 @@ int comm_wait_devs(rm_ctx* c) {
       if (done[i]) continue;
       rm_ctx* m = ms[i];
       (void)hipSetDevice(m->device);
-      const hipError_t q = hipStreamQuery(m->stream);
+      // the render stream and, after a batch, the gather stream
+      hipError_t q = hipStreamQuery(m->stream);
+      if (q == hipSuccess && m->gstream) q = hipStreamQuery(m->gstream);
       if (q == hipSuccess) {
         done[i] = true;
         continue;
@@ -253,7 +278,9 @@ int comm_wait_devs(rm_ctx* c) {
 // Waits for an RCCL call that returned ncclInProgress (non-blocking communicator).
 int comm_enqueued(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
   if (e == ncclSuccess) return RM_OK;
-  if (e != ncclInProgress) return nccl_fail(c, r, e, what);
+  // an enqueue error aborts the communicator (rm_api.h: RM_ERR_COMM means aborted);
+  // a partial group may already have launched gathers that would wait forever
+  if (e != ncclInProgress) return comm_abort(c, std::string(what) + ": " + r->GetErrorString(e));
   std::vector<ncclComm_t> cs;
   for (rm_ctx* m : comm_members(c))
     if (m->comm) cs.push_back(m->comm);
@@ -511,11 +538,28 @@ void free_all(rm_ctx* c) {
     if (p) (void)hipFree(p);
   c->d_gathered = c->d_frame = nullptr;
   c->d_gathered32 = c->d_frame32 = nullptr;
+  if (c->gstream) (void)hipStreamSynchronize(c->gstream);
+  for (uint8_t* p : c->ring8) (void)hipFree(p);
+  for (float* p : c->ring32) (void)hipFree(p);
+  c->ring8.clear();
+  c->ring32.clear();
+  for (auto& b : c->bslot) {
+    if (b.send8) (void)hipFree(b.send8);
+    if (b.send32) (void)hipFree(b.send32);
+    if (b.rendered) (void)hipEventDestroy(b.rendered);
+    if (b.freed) (void)hipEventDestroy(b.freed);
+    b = rm_ctx::BatchSlot();
+  }
+  if (c->gdone) (void)hipEventDestroy(c->gdone);
+  c->gdone = nullptr;
+  if (c->gstream) (void)hipStreamDestroy(c->gstream);
+  c->gstream = nullptr;
   for (auto& p : c->ev_pool) {
     (void)hipEventDestroy(p.first);
     (void)hipEventDestroy(p.second);
   }
   c->ev_pool.clear();
+  c->ev_frames.clear();
   for (hipEvent_t& e : c->ph) {
     if (e) (void)hipEventDestroy(e);
     e = nullptr;
@@ -666,8 +710,16 @@ int create_multi(rm_ctx** out, const rm_config* cfg) {
   }
   for (int i = 0; i < n; ++i) {
     if ((rc = comm_attach(c->subs[i], comms[i], i, n, true, true)) != RM_OK) {
+      //  abort every member, attached or not, and detach them, so the
+      // teardown below neither finalizes a half-aborted group (and waits out the
+      // deadline) nor leaks comms[i]
       c->err = c->subs[i]->err;
-      for (int j = i + 1; j < n; ++j) (void)r->CommAbort(comms[j]);
+      for (int j = 0; j < n; ++j) {
+        (void)hipSetDevice(devs[j]);
+        (void)r->CommAbort(comms[j]);
+        c->subs[j]->comm = nullptr;
+        c->subs[j]->own_comm = false;
+      }
       return bail(rc);
     }
     c->subs[i]->comm_timeout_ms = c->comm_timeout_ms;
@@ -752,6 +804,7 @@ int rm_config_init(rm_config* cfg, int32_t width, int32_t height) {
   if (!cfg) return RM_ERR_INVALID;
   std::memset(cfg, 0, sizeof *cfg);
   cfg->struct_size = (uint32_t)sizeof(rm_config);
+  cfg->magic = RM_CONFIG_MAGIC;
   cfg->width = width;
   cfg->height = height;
   cfg->device = -1;
@@ -765,11 +818,11 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
   *out = nullptr;
   // A host built against an older rm_api.h passes a smaller struct without this
   // field (its first word is the width): refuse it rather than read past its end.
-  if (cfg->struct_size != (uint32_t)sizeof(rm_config))
+  if (cfg->struct_size != (uint32_t)sizeof(rm_config) || cfg->magic != RM_CONFIG_MAGIC)
     return fail(nullptr, RM_ERR_INVALID,
                 "rm_create: rm_config.struct_size must be sizeof(rm_config) = " +
-                    std::to_string(sizeof(rm_config)) + " (rm_config_init; API version " +
-                    std::to_string(RM_API_VERSION) + ")");
+                    std::to_string(sizeof(rm_config)) + " and rm_config.magic RM_CONFIG_MAGIC (rm_config_init; "
+                    "API version " + std::to_string(RM_API_VERSION) + ")");
   if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65536 || cfg->height > 65536)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: width/height must be in 1..65536");
   if (cfg->ngpus < 0 || cfg->ngpus > 64)
@@ -885,6 +938,7 @@ void rm_destroy(rm_ctx* ctx) {
   // wait aborts the communicator on its deadline, and the aborted gather quits
   if (has_comm(ctx) && !ctx->comm_failed && !ctx->group_member) (void)comm_wait(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
   free_all(ctx);
   delete ctx;
 }
@@ -969,7 +1023,21 @@ int timing_events(rm_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
   }
   *e0 = c->ev_pool[c->ev_used].first;
   *e1 = c->ev_pool[c->ev_used].second;
+  if (c->ev_frames.size() < c->ev_pool.size()) c->ev_frames.resize(c->ev_pool.size(), 1);
+  c->ev_frames[c->ev_used] = 1;
   c->ev_used++;
+  return RM_OK;
+}
+
+// A plain dispatch after a batch on a communicator context: its render may
+// write the image the batch's assembly writes, and its gather must follow the
+// batch's on the communicator, so the context's stream waits for the gather
+// stream's last batch (rm_dispatch_frames).
+int order_after_batch(rm_ctx* c) {
+  c->batch_n = 1;
+  if (!c->gdone_pending) return RM_OK;
+  RM_HIP(c, hipStreamWaitEvent(c->stream, c->gdone, 0));
+  c->gdone_pending = false;
   return RM_OK;
 }
 
@@ -977,6 +1045,7 @@ int timing_events(rm_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
 int render_launch(rm_ctx* c) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
+  if ((rc = order_after_batch(c)) != RM_OK) return rc;
   if (c->cfg.counters) {
     RM_HIP(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
   }
@@ -998,10 +1067,10 @@ int graph_frame(rm_ctx* c);
 
 // Phase k of the frame (0 render start, 1 render end, 2 gather end, 3 assembly
 // end) on the context's stream, when timing is on (rm_frame_phases).
-int phase(rm_ctx* c, int k) {
+int phase(rm_ctx* c, int k, hipStream_t st = nullptr) {
   if (!c->timing) return RM_OK;
   if (!c->ph[k]) RM_HIP(c, hipEventCreate(&c->ph[k]));
-  RM_HIP(c, hipEventRecord(c->ph[k], c->stream));
+  RM_HIP(c, hipEventRecord(c->ph[k], st ? st : c->stream));
   return RM_OK;
 }
 
@@ -1023,12 +1092,18 @@ int multi_frame(rm_ctx* c, bool graph) {
     if (timed && (rc = phase(s, 1)) != RM_OK) return fail(c, rc, s->err);
   }
   ncclResult_t e = r->GroupStart();
-  if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclGroupStart");
+  if (e != ncclSuccess) return comm_abort(c, std::string("ncclGroupStart: ") + r->GetErrorString(e));
+  std::string why;
   for (rm_ctx* s : c->subs) {
-    if ((rc = set_device(s)) != RM_OK || (rc = comm_gather(s)) != RM_OK) break;
+    if ((rc = set_device(s)) != RM_OK || (rc = comm_gather(s)) != RM_OK) {
+      why = s->err;
+      break;
+    }
   }
   e = r->GroupEnd();
-  if (rc != RM_OK) return fail(c, rc, c->subs.empty() ? "" : c->subs[0]->err);
+  // a partial group: the gathers already queued on some devices can never
+  // complete, so the communicator is aborted (not left to the deadline)
+  if (rc != RM_OK) return comm_abort(c, "gather (partial group): " + why);
   if ((rc = comm_enqueued(c, r, e, "ncclGroupEnd (gather)")) != RM_OK) return rc;
   rm_ctx* s0 = c->subs[0];
   if ((rc = set_device(s0)) != RM_OK) return fail(c, rc, s0->err);
@@ -1041,6 +1116,245 @@ int multi_frame(rm_ctx* c, bool graph) {
   return RM_OK;
 }
 
+
+// ---- frame batches (rm_dispatch_frames) ------------------------------------------
+// One launch renders n frames (grid.z = frame, rm_kernels.hip k_*_frames), so
+// the waves of frame k + 1 fill the SIMDs that frame k's longest waves leave
+// idle.  Frames 0..n-2 go to a ring of images the context keeps, frame n-1 to
+// the context's image, so afterwards the context reads as after n rm_dispatch
+// calls.  On a communicator context the n shards of one rank go to a batch slot
+// and move in ONE ncclGather on the gather stream; rank 0 assembles the n
+// frames there.  Two slots alternate, so batch j + 1 renders while batch j
+// gathers, and all of a communicator's collectives stay on one stream in issue
+// order.
+
+// Images for frames 0..n-2 of a batch, `rows` x width, per enabled format.
+int ensure_ring(rm_ctx* c, int n, int rows) {
+  const size_t px = (size_t)rows * (size_t)c->cfg.width;
+  while ((c->cfg.outputs & RM_OUT_RGBA8) && (int)c->ring8.size() < n - 1) {
+    uint8_t* p = nullptr;
+    RM_HIP(c, hipMalloc(&p, px * 4));
+    c->ring8.push_back(p);
+  }
+  while ((c->cfg.outputs & RM_OUT_RGBA32F) && (int)c->ring32.size() < n - 1) {
+    float* p = nullptr;
+    RM_HIP(c, hipMalloc(&p, px * 16));
+    c->ring32.push_back(p);
+  }
+  return RM_OK;
+}
+
+// The frame constants of frames[0..n) with their output pointers, launched in
+// runs of one AA setting (one grid per run); a runtime scene table renders one
+// launch per frame.  out8(k) / out32(k): frame k's destinations.
+// (C++ linkage: this block sits inside the C-ABI's extern "C")
+extern "C++" template <class O8, class O32>
+int launch_batch(rm_ctx* c, const rm_uniforms* u, int n, O8 out8, O32 out32) {
+  static thread_local rmd::FrameBatch B;  // 11.5 KB of kernel arguments
+  int m = 0;
+  auto flush = [&]() -> int {
+    if (m == 0) return RM_OK;
+    const hipError_t e = rm::launch_frames(B, m, c->stream);
+    m = 0;
+    if (e != hipSuccess) return hip_fail(c, e, "batch launch");
+    return RM_OK;
+  };
+  int rc = RM_OK;
+  for (int k = 0; k < n; ++k) {
+    c->u = u[k];
+    rmd::Frame F = make_frame(c);
+    F.rgba8 = out8(k);
+    F.rgba32f = out32(k);
+    F.sdf_counts = nullptr;
+    F.counters = nullptr;
+    if (c->nprims) {
+      const hipError_t e = c->jit ? rm::launch_table_jit(c->jit, F, false, c->stream)
+                                  : rm::launch_table(F, false, c->stream, table_slots(c));
+      if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
+      continue;
+    }
+    if (m > 0 && B.f[0].aa != F.aa && (rc = flush()) != RM_OK) return rc;
+    B.f[m++] = F;
+  }
+  return flush();
+}
+
+int plain_batch(rm_ctx* c, const rm_uniforms* u, int n) {
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if ((rc = order_after_batch(c)) != RM_OK) return rc;
+  if ((rc = ensure_ring(c, n, c->rows)) != RM_OK) return rc;
+  uint8_t* dst8 = render_dst(c);
+  float* dst32 = render_dst32(c);
+  hipEvent_t e0, e1;
+  if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
+  if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
+  if ((rc = phase(c, 0)) != RM_OK) return rc;
+  rc = launch_batch(
+      c, u, n, [&](int k) { return dst8 ? (k < n - 1 ? c->ring8[k] : dst8) : nullptr; },
+      [&](int k) { return dst32 ? (k < n - 1 ? c->ring32[k] : dst32) : nullptr; });
+  if (rc != RM_OK) return rc;
+  if ((rc = phase(c, 1)) != RM_OK) return rc;
+  if (e1) {
+    RM_HIP(c, hipEventRecord(e1, c->stream));
+    c->ev_frames[c->ev_used - 1] = n;
+  }
+  if (c->timing) {
+    c->ph_recorded = true;
+    c->ph_comm = false;
+  }
+  c->batch_n = n;
+  c->dispatched = true;
+  return RM_OK;
+}
+
+// A communicator context's batch slot holding n frames: this rank's shards
+// ([n][rows][width]), or on rank 0 the whole gather buffer ([nranks][n][rows]
+// [width]).  Re-allocated only for a longer batch, after the slot's last
+// gather has read it.
+int slot_alloc(rm_ctx* c, rm_ctx::BatchSlot& b, int n) {
+  if (!b.rendered) RM_HIP(c, hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
+  if (!b.freed) RM_HIP(c, hipEventCreateWithFlags(&b.freed, hipEventDisableTiming));
+  if (b.cap >= n) return RM_OK;
+  if (b.pending) RM_HIP(c, hipEventSynchronize(b.freed));
+  RM_HIP(c, hipStreamSynchronize(c->stream));
+  if (b.send8) (void)hipFree(b.send8);
+  if (b.send32) (void)hipFree(b.send32);
+  b.send8 = nullptr;
+  b.send32 = nullptr;
+  b.cap = 0;
+  const size_t px = (size_t)c->rows * (size_t)c->cfg.width * (size_t)n * (comm_root(c) ? c->cranks : 1);
+  if (c->cfg.outputs & RM_OUT_RGBA8) RM_HIP(c, hipMalloc(&b.send8, px * 4));
+  if (c->cfg.outputs & RM_OUT_RGBA32F) RM_HIP(c, hipMalloc(&b.send32, px * 16));
+  b.cap = n;
+  return RM_OK;
+}
+
+// Step 1 of a communicator batch: this rank's n shards in one launch, on the
+// context's stream, into the next slot.
+int batch_render(rm_ctx* c, const rm_uniforms* u, int n) {
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  if ((rc = order_after_batch(c)) != RM_OK) return rc;
+  if (!c->gstream) {
+    RM_HIP(c, hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    RM_HIP(c, hipEventCreateWithFlags(&c->gdone, hipEventDisableTiming));
+  }
+  rm_ctx::BatchSlot& b = c->bslot[c->bnext];
+  if ((rc = slot_alloc(c, b, n)) != RM_OK) return rc;
+  if (comm_root(c) && (rc = ensure_ring(c, n, c->cfg.height)) != RM_OK) return rc;
+  // the slot's previous batch (two batches ago) has been gathered and assembled
+  if (b.pending) RM_HIP(c, hipStreamWaitEvent(c->stream, b.freed, 0));
+  const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
+  hipEvent_t e0, e1;
+  if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
+  if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
+  if ((rc = phase(c, 0)) != RM_OK) return rc;
+  rc = launch_batch(
+      c, u, n, [&](int k) { return b.send8 ? b.send8 + (size_t)k * px * 4 : nullptr; },
+      [&](int k) { return b.send32 ? b.send32 + (size_t)k * px * 4 : nullptr; });
+  if (rc != RM_OK) return rc;
+  if ((rc = phase(c, 1)) != RM_OK) return rc;
+  if (e1) {
+    RM_HIP(c, hipEventRecord(e1, c->stream));
+    c->ev_frames[c->ev_used - 1] = n;
+  }
+  RM_HIP(c, hipEventRecord(b.rendered, c->stream));
+  return RM_OK;
+}
+
+// Step 2 (inside an RCCL group): the slot's n shards to rank 0 in one gather
+// per format, on the gather stream once the render is done.
+ncclResult_t batch_gather(rm_ctx* c, const rm::Rccl* r, int n) {
+  if (set_device(c) != RM_OK) return ncclUnhandledCudaError;
+  rm_ctx::BatchSlot& b = c->bslot[c->bnext];
+  if (hipStreamWaitEvent(c->gstream, b.rendered, 0) != hipSuccess) return ncclUnhandledCudaError;
+  const size_t count = (size_t)c->rows * (size_t)c->cfg.width * 4 * (size_t)n;  // 4 B or 4 floats per px
+  const bool root = comm_root(c);
+  ncclResult_t e = ncclSuccess;
+  if (b.send8) e = r->Gather(b.send8, root ? b.send8 : nullptr, count, ncclUint8, 0, c->comm, c->gstream);
+  if ((e == ncclSuccess || e == ncclInProgress) && b.send32)
+    e = r->Gather(b.send32, root ? b.send32 : nullptr, count, ncclFloat32, 0, c->comm, c->gstream);
+  return e;
+}
+
+// Step 3, on the gather stream: rank 0 assembles the n frames (frames 0..n-2
+// into its ring, frame n-1 into its image); another rank copies its last shard
+// into its image, so the context reads as after n rm_dispatch calls.
+int batch_finish(rm_ctx* c, int n) {
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  rm_ctx::BatchSlot& b = c->bslot[c->bnext];
+  const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
+  if ((rc = phase(c, 2, c->gstream)) != RM_OK) return rc;
+  if (comm_root(c)) {
+    const int W = c->cfg.width, H = c->cfg.height, rb = c->cfg.row_block;
+    const size_t stride = (size_t)n * (size_t)c->rows;  // rows between two ranks' blocks
+    for (int k = 0; k < n; ++k) {
+      if (b.send8) {
+        void* dst = k < n - 1 ? (void*)c->ring8[k] : (void*)image_rgba8(c);
+        const hipError_t e = rm::launch_unshard(b.send8 + (size_t)k * px * 4, dst, W, H, rb, c->cranks, c->rows,
+                                                c->gstream, stride);
+        if (e != hipSuccess) return hip_fail(c, e, "unshard launch (batch)");
+      }
+      if (b.send32) {
+        void* dst = k < n - 1 ? (void*)c->ring32[k] : (void*)c->d_frame32;
+        const hipError_t e = rm::launch_unshard(b.send32 + (size_t)k * px * 4, dst, W * 4, H, rb, c->cranks,
+                                                c->rows, c->gstream, stride);
+        if (e != hipSuccess) return hip_fail(c, e, "unshard launch (batch, RGBA32F)");
+      }
+    }
+  } else {
+    if (b.send8 && render_dst(c))
+      RM_HIP(c, hipMemcpyAsync(render_dst(c), b.send8 + (size_t)(n - 1) * px * 4, px * 4, hipMemcpyDeviceToDevice,
+                               c->gstream));
+    if (b.send32 && render_dst32(c))
+      RM_HIP(c, hipMemcpyAsync(render_dst32(c), b.send32 + (size_t)(n - 1) * px * 4, px * 16,
+                               hipMemcpyDeviceToDevice, c->gstream));
+  }
+  if ((rc = phase(c, 3, c->gstream)) != RM_OK) return rc;
+  RM_HIP(c, hipEventRecord(b.freed, c->gstream));
+  b.pending = true;
+  RM_HIP(c, hipEventRecord(c->gdone, c->gstream));
+  c->gdone_pending = true;
+  if (c->timing) {
+    c->ph_recorded = true;
+    c->ph_comm = true;
+  }
+  c->blast = c->bnext;
+  c->bnext ^= 1;
+  c->batch_n = n;
+  c->comm_warm = true;
+  c->dispatched = true;
+  return RM_OK;
+}
+
+// One rank's batch (rm_comm_init), or a multi-GPU context's (every device
+// renders, one group gathers, device 0 assembles).
+int comm_batch(rm_ctx* c, const rm_uniforms* u, int n) {
+  if (c->comm_failed) return comm_dead(c);
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  const std::vector<rm_ctx*> ms = comm_members(c);
+  int rc = RM_OK;
+  for (rm_ctx* m : ms)
+    if ((rc = batch_render(m, u, n)) != RM_OK) return m == c ? rc : fail(c, rc, m->err);
+  ncclResult_t e = r->GroupStart();
+  if (e != ncclSuccess) return comm_abort(c, std::string("ncclGroupStart: ") + r->GetErrorString(e));
+  for (rm_ctx* m : ms) {
+    e = batch_gather(m, r, n);
+    if (e != ncclSuccess && e != ncclInProgress) break;
+  }
+  const ncclResult_t eg = r->GroupEnd();
+  if (e == ncclSuccess || e == ncclInProgress) e = eg;
+  if ((rc = comm_enqueued(c, r, e, "ncclGather (batch)")) != RM_OK) return rc;
+  for (rm_ctx* m : ms)
+    if ((rc = batch_finish(m, n)) != RM_OK) return m == c ? rc : fail(c, rc, m->err);
+  c->batch_n = n;
+  c->dispatched = true;
+  return RM_OK;
+}
 }  // namespace
 
 int rm_dispatch(rm_ctx* c) {
@@ -1064,6 +1378,23 @@ int rm_dispatch(rm_ctx* c) {
     c->ph_comm = comm;
   }
   return RM_OK;
+}
+
+int rm_dispatch_frames(rm_ctx* c, const rm_uniforms* u, int32_t n) {
+  if (!c || !u) return RM_ERR_INVALID;
+  if (n < 1 || n > RM_MAX_BATCH)
+    return fail(c, RM_ERR_INVALID, "rm_dispatch_frames: n must be in 1.." + std::to_string(RM_MAX_BATCH));
+  for (int k = 0; k < n; ++k) {
+    const int rc = check_uniforms(c, u[k]);
+    if (rc != RM_OK) return rc;
+  }
+  if (c->cfg.counters) return fail(c, RM_ERR_STATE, "rm_dispatch_frames: not available with counters");
+  int rc;
+  if (has_comm(c) && !c->group_member) rc = comm_batch(c, u, n);
+  else rc = plain_batch(c, u, n);
+  c->u = u[n - 1];
+  for (rm_ctx* s : c->subs) s->u = u[n - 1];
+  return rc;
 }
 
 int rm_synchronize(rm_ctx* c) {
@@ -1119,6 +1450,37 @@ int rm_read_rgba8(rm_ctx* c, uint8_t* dst, size_t row_pitch, int flip_y) {
 int rm_read_rgba32f(rm_ctx* c, float* dst, size_t row_pitch, int flip_y) {
   if (!c) return RM_ERR_INVALID;
   return read_image(c, image_rgba32f(c), 16, dst, row_pitch, flip_y);
+}
+
+// Frame k of the last batch: the context's image for k = n-1; else rank 0's
+// (or a plain context's) ring, or another rank's shard in the batch's slot.
+static int read_frame(rm_ctx* c, int32_t k, bool f32, void* dst, size_t row_pitch, int flip_y) {
+  if (!c) return RM_ERR_INVALID;
+  rm_ctx* t = c->subs.empty() ? c : c->subs[0];
+  const int n = t->batch_n;
+  if (k < 0 || k >= n)
+    return fail(c, RM_ERR_INVALID, "frame " + std::to_string(k) + " of a batch of " + std::to_string(n));
+  if (k == n - 1) return f32 ? rm_read_rgba32f(c, (float*)dst, row_pitch, flip_y)
+                             : rm_read_rgba8(c, (uint8_t*)dst, row_pitch, flip_y);
+  const void* dev;
+  if (t->comm && !comm_root(t)) {
+    const rm_ctx::BatchSlot& b = t->bslot[t->blast];
+    const size_t px = (size_t)t->rows * (size_t)t->cfg.width;
+    dev = f32 ? (const void*)(b.send32 ? b.send32 + (size_t)k * px * 4 : nullptr)
+              : (const void*)(b.send8 ? b.send8 + (size_t)k * px * 4 : nullptr);
+  } else {
+    dev = f32 ? (const void*)((size_t)k < t->ring32.size() ? t->ring32[k] : nullptr)
+              : (const void*)((size_t)k < t->ring8.size() ? t->ring8[k] : nullptr);
+  }
+  return read_image(c, dev, f32 ? 16 : 4, dst, row_pitch, flip_y);
+}
+
+int rm_read_frame_rgba8(rm_ctx* c, int32_t k, uint8_t* dst, size_t row_pitch, int flip_y) {
+  return read_frame(c, k, false, dst, row_pitch, flip_y);
+}
+
+int rm_read_frame_rgba32f(rm_ctx* c, int32_t k, float* dst, size_t row_pitch, int flip_y) {
+  return read_frame(c, k, true, dst, row_pitch, flip_y);
 }
 
 int rm_get_counters(rm_ctx* c, rm_counters* out) {
@@ -1231,6 +1593,7 @@ int graph_frame(rm_ctx* c) {
   if (c->comm_failed) return comm_dead(c);
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
+  if ((rc = order_after_batch(c)) != RM_OK) return rc;
   rmd::Frame F = make_frame(c);
   const bool comm = c->comm && !c->group_member;
   if (comm && !c->comm_warm) {
@@ -1428,7 +1791,7 @@ int rm_kernel_time_ms(rm_ctx* c, double* total_ms, int64_t* launches, int reset)
     float ms = 0.0f;
     RM_HIP(c, hipEventElapsedTime(&ms, c->ev_pool[i].first, c->ev_pool[i].second));
     c->total_ms += ms;
-    c->launches++;
+    c->launches += i < c->ev_frames.size() ? c->ev_frames[i] : 1;  // a batch counts its frames
   }
   c->ev_used = 0;
   if (total_ms) *total_ms = c->total_ms;
@@ -1457,6 +1820,9 @@ int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
   if (!c || !id) return RM_ERR_INVALID;
   if (!c->subs.empty()) return fail(c, RM_ERR_STATE, "a multi-GPU context has its own communicator");
   if (c->comm) return fail(c, RM_ERR_STATE, "the context already has a communicator");
+  // an aborted context can only be destroyed (rm_api.h); a second init would
+  // re-attach without freeing its gather buffers
+  if (c->comm_failed) return comm_dead(c);
   if (nranks < 1 || rank < 0 || rank >= nranks)
     return fail(c, RM_ERR_INVALID, "rm_comm_init: rank must be in 0..nranks-1");
   const int ns = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
@@ -1544,6 +1910,44 @@ int rm_comm_info(const rm_ctx* c, int32_t* rank, int32_t* nranks, int32_t* ngpus
   if (rank) *rank = c->crank;
   if (nranks) *nranks = c->subs.empty() ? c->cranks : (int32_t)c->subs.size();
   if (ngpus) *ngpus = c->subs.empty() ? 1 : (int32_t)c->subs.size();
+  return RM_OK;
+}
+
+int rm_comm_rccl_info(rm_ctx* c, int32_t* count, int32_t* user_rank, int32_t* hip_device, int32_t* version) {
+  if (!c) return RM_ERR_INVALID;
+  if (count) *count = 0;
+  if (user_rank) *user_rank = -1;
+  if (hip_device) *hip_device = -1;
+  if (version) *version = 0;
+  if (c->comm_failed) return comm_dead(c);
+  if (!has_comm(c)) return RM_OK;
+  std::string err;
+  const rm::Rccl* r = rm::rccl(&err);
+  if (!r) return fail(c, RM_ERR_COMM, err);
+  int v = 0;
+  if (version && r->GetVersion(&v) == ncclSuccess) *version = v;
+  // every member communicator as RCCL formed it: a multi-GPU context's device i
+  // must be user rank i of ngpus, a rank's communicator rank crank of cranks
+  const std::vector<rm_ctx*> ms = comm_members(c);
+  for (size_t i = 0; i < ms.size(); ++i) {
+    int n = 0, ur = -1, dev = -1;
+    ncclResult_t e = r->CommCount(ms[i]->comm, &n);
+    if (e == ncclSuccess) e = r->CommUserRank(ms[i]->comm, &ur);
+    if (e == ncclSuccess) e = r->CommCuDevice(ms[i]->comm, &dev);
+    if (e != ncclSuccess) return nccl_fail(c, r, e, "ncclCommCount / ncclCommUserRank / ncclCommCuDevice");
+    const int want_n = c->subs.empty() ? c->cranks : (int)ms.size();
+    const int want_r = c->subs.empty() ? c->crank : (int)i;
+    if (n != want_n || ur != want_r || dev != ms[i]->device)
+      return fail(c, RM_ERR_COMM, "RCCL reports rank " + std::to_string(ur) + " of " + std::to_string(n) +
+                                      " on device " + std::to_string(dev) + " for a member set up as rank " +
+                                      std::to_string(want_r) + " of " + std::to_string(want_n) + " on device " +
+                                      std::to_string(ms[i]->device));
+    if (i == 0) {
+      if (count) *count = n;
+      if (user_rank) *user_rank = ur;
+      if (hip_device) *hip_device = dev;
+    }
+  }
   return RM_OK;
 }
 

@@ -50,6 +50,9 @@ void load() {
   sym("ncclGather", g_rccl.Gather);
   sym("ncclGetErrorString", g_rccl.GetErrorString);
   sym("ncclGetVersion", g_rccl.GetVersion);
+  sym("ncclCommCount", g_rccl.CommCount);
+  sym("ncclCommUserRank", g_rccl.CommUserRank);
+  sym("ncclCommCuDevice", g_rccl.CommCuDevice);
   if (ok) g_ok = &g_rccl;
 }
 

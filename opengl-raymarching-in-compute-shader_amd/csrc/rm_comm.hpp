@@ -27,6 +27,11 @@ struct Rccl {
   decltype(&ncclGather) Gather;
   decltype(&ncclGetErrorString) GetErrorString;
   decltype(&ncclGetVersion) GetVersion;
+  // what the communicator itself reports (rm_comm_rccl_info): the rank count and
+  // this member's rank as RCCL formed them, and the device it is bound to
+  decltype(&ncclCommCount) CommCount;
+  decltype(&ncclCommUserRank) CommUserRank;
+  decltype(&ncclCommCuDevice) CommCuDevice;
 };
 
 // The loaded entry points, or nullptr with *err set (no RCCL on this host, or one

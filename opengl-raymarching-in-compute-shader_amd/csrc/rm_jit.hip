@@ -9,14 +9,20 @@
 // arithmetic is the same source under the same flags (-ffp-contract=off), so the
 // image equals the generic table kernel's bit for bit (tests/test_gpu_scene.py).
 //
-// Register bound per table: the kernels are compiled for the most waves per SIMD
-// (8, 7 or 6: __launch_bounds__(64, w), RM_TABLE_MIN_WAVES) at which the
-// production kernels need no scratch (private segment 0 in their kernel
-// descriptors).  A bound the table's unrolled code does not fit spills to
-// scratch, and the spill traffic grows with the table (a 30-entry table spills
-// 100+ VGPRs per kernel even at 4 waves): a table that fits none of the three
-// is not specialised, and renders with the generic (LDS-staged) kernel, whose
-// registers do not grow with the table.
+// Register bound per table: the kernels run at the most waves per SIMD (8, 7 or
+// 6) at which the production kernels need no scratch (private segment 0 in their
+// kernel descriptors).  One compile usually decides it (round 4, VERDICT r03
+// #6): the table is compiled without an occupancy bound (RM_TABLE_MIN_WAVES = 1),
+// the descriptors give each production kernel's VGPR allocation, and a kernel
+// that allocates at most 512 / w registers already runs at w waves with no
+// scratch.  The reference scene's kernels allocate 72 VGPRs unbounded: 7 waves,
+// the bound the round-2 ladder (8, then 7) found with two compiles; bounded to 8
+// waves they spill.  Only a table whose kernels need more than 80 registers
+// unbounded is compiled once more, bounded to 6 waves, and that build is kept
+// if it needs no scratch; one that spills even there (a 30-entry table spills
+// 100+ VGPRs at 4 waves) is not specialised and renders with the generic
+// (LDS-staged) kernel, whose registers do not grow with the table.  RM_JIT_LOG=1
+// prints one line per hiprtc compile (stderr).
 //
 // Modules are cached per (device, table words) for the life of the process:
 // contexts rendering the same table (frames in flight) share one compile.
@@ -25,6 +31,7 @@
 #include <hip/hiprtc.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -48,15 +55,17 @@ const char* const kNames[2][2] = {{"rmd::k_table_pixel<false>", "rmd::k_table_pi
 
 namespace rm {
 
-// private_segment_fixed_size of kernel `name` (its .kd kernel descriptor: u32 at
-// offset 4) in an AMDGPU code object (ELF64); -1 when not found.
-long kernel_private_size(const std::vector<char>& code, const std::string& name) {
-  if (code.size() < sizeof(Elf64_Ehdr)) return -1;
+// The kernel descriptor `name`.kd of an AMDGPU code object (ELF64): the
+// private_segment_fixed_size (u32 at offset 4; scratch bytes per lane) and the
+// VGPR allocation per lane (compute_pgm_rsrc1 at offset 48, bits 5:0 =
+// allocation / 8 - 1 on gfx950, VGPRs and AGPRs together).  false when absent.
+bool kernel_desc(const std::vector<char>& code, const std::string& name, long* priv, int* vgprs) {
+  if (code.size() < sizeof(Elf64_Ehdr)) return false;
   const char* base = code.data();
   const auto* eh = reinterpret_cast<const Elf64_Ehdr*>(base);
   if (std::memcmp(eh->e_ident, ELFMAG, SELFMAG) != 0 || eh->e_shoff == 0 ||
       eh->e_shoff + (size_t)eh->e_shnum * sizeof(Elf64_Shdr) > code.size())
-    return -1;
+    return false;
   const auto* sh = reinterpret_cast<const Elf64_Shdr*>(base + eh->e_shoff);
   const std::string kd = name + ".kd";
   for (int i = 0; i < eh->e_shnum; ++i) {
@@ -68,14 +77,24 @@ long kernel_private_size(const std::vector<char>& code, const std::string& name)
       if (sym[k].st_name >= strs.sh_size || sym[k].st_shndx >= eh->e_shnum) continue;
       if (kd != base + strs.sh_offset + sym[k].st_name) continue;
       const Elf64_Shdr& sec = sh[sym[k].st_shndx];
-      const size_t off = sec.sh_offset + (sym[k].st_value - sec.sh_addr) + 4;
-      if (off + 4 > code.size()) return -1;
-      uint32_t v;
-      std::memcpy(&v, base + off, 4);
-      return (long)v;
+      const size_t off = sec.sh_offset + (sym[k].st_value - sec.sh_addr);
+      if (off + 64 > code.size()) return false;
+      uint32_t p, rsrc1;
+      std::memcpy(&p, base + off + 4, 4);
+      std::memcpy(&rsrc1, base + off + 48, 4);
+      *priv = (long)p;
+      *vgprs = (int)((rsrc1 & 0x3fu) + 1u) * 8;
+      return true;
     }
   }
-  return -1;
+  return false;
+}
+
+// Waves per SIMD a kernel allocating `vgprs` registers per lane can hold (512
+// per SIMD lane, granule 8), capped at 8.
+int waves_for(int vgprs) {
+  const int w = vgprs > 0 ? 512 / vgprs : 8;
+  return w < 8 ? w : 8;
 }
 
 // hiprtc: the table kernels for words[0..scene_words(n)) as a code object for
@@ -120,6 +139,8 @@ int jit_compile_waves(const uint32_t* words, int32_t n, const std::string& arch,
 #endif
   const char* opts[] = {a.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
                         "-DRM_TABLE_STATIC=1", w.c_str(), RM_JIT_EXTRA};
+  if (const char* lg = std::getenv("RM_JIT_LOG"); lg && *lg == '1')
+    std::fprintf(stderr, "rm_jit: hiprtc compile, %d-entry table, occupancy bound %d waves\n", n, min_waves);
   const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
@@ -149,35 +170,64 @@ int jit_compile_waves(const uint32_t* words, int32_t n, const std::string& arch,
   return RM_OK;
 }
 
+// Waves per SIMD the production kernels (k_table_*<false>; lowered[0],
+// lowered[2]) of a compiled code object run at, or 0 when either needs scratch;
+// -1 (with err) when a descriptor is missing: that is an error, not a spill, as
+// silently falling back to the generic kernel would hide a code-object layout
+// change.
+int production_waves(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
+  int w = 8;
+  for (int k : {0, 2}) {
+    long priv = -1;
+    int vg = 0;
+    if (!kernel_desc(c, l[k], &priv, &vg)) {
+      err = "rm_scene_specialize: kernel descriptor " + l[k] + ".kd not found in the compiled code object";
+      return -1;
+    }
+    if (priv != 0) return 0;
+    const int wk = waves_for(vg);
+    w = wk < w ? wk : w;
+  }
+  return w;
+}
+
 // The table kernels at the most waves per SIMD (8, 7, 6) whose production
-// kernels (k_table_*<false>; lowered[0], lowered[2]) use no scratch: *waves is
-// that bound, or 0 (code left empty) when every bound spills.  The ladder stops
-// at the first bound that fits, so the common case (the reference scene fits 7)
-// pays two compiles; a missing kernel descriptor is RM_ERR_HIP.
+// kernels use no scratch: *waves is that, or 0 (code left empty) when none
+// fits.  One compile without an occupancy bound decides every table whose
+// kernels fit 80 registers (above); a second, bounded to 6 waves, runs only for
+// a larger one.
 int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::vector<char>& code,
                 std::vector<std::string>& lowered, std::string& err, int* waves) {
   if (waves) *waves = 0;
   code.clear();
-  for (int mw = 8; mw >= 6; --mw) {
-    std::vector<char> c;
-    std::vector<std::string> l;
-    const int rc = jit_compile_waves(words, n, arch, mw, c, l, err);
+  std::vector<char> c;
+  std::vector<std::string> l;
+  int rc = jit_compile_waves(words, n, arch, 1, c, l, err);
+  if (rc != RM_OK) return rc;
+  int w = production_waves(c, l, err);
+  if (w < 0) return RM_ERR_HIP;
+  if (w >= 6) {  // usable as it is
+    code.swap(c);
+    lowered.swap(l);
+  }
+  if (w < 6) {
+    // more than 80 registers unbounded: one compile bounded to 6 waves, kept
+    // when it needs no scratch
+    rc = jit_compile_waves(words, n, arch, 6, c, l, err);
     if (rc != RM_OK) return rc;
-    const long p0 = kernel_private_size(c, l[0]), p2 = kernel_private_size(c, l[2]);
-    if (p0 < 0 || p2 < 0) {
-      // a descriptor we cannot read is an error, not a spill: silently falling
-      // back to the generic kernel would hide a code-object layout change
-      err = "rm_scene_specialize: kernel descriptor " + (p0 < 0 ? l[0] : l[2]) +
-            ".kd not found in the compiled code object";
-      return RM_ERR_HIP;
-    }
-    if (p0 == 0 && p2 == 0) {
+    const int wb = production_waves(c, l, err);
+    if (wb < 0) return RM_ERR_HIP;
+    if (wb >= 6) {
       code.swap(c);
       lowered.swap(l);
-      if (waves) *waves = mw;
-      break;
+      w = wb;
     }
   }
+  if (w < 6) {
+    code.clear();
+    w = 0;
+  }
+  if (waves) *waves = w;
   return RM_OK;
 }
 

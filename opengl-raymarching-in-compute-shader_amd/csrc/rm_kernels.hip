@@ -530,22 +530,39 @@ __global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
 }
 #endif
 
-// Reassemble [nshards][rows_cap][width] packed shard images into the frame.
-// One grid row per frame row: the source row (shard, local row) is computed once
-// per workgroup in scalar registers; lanes copy 16 B (4 pixels) each when rows
-// are 16-B aligned (width % 4 == 0 and both images 16-B aligned), one pixel
-// otherwise.
+// Frame batches (rm_dispatch_frames): grid.z = the frame.  The hardware
+// dispatches workgroups in x, y, z order, so the slow middle rows of frame z + 1
+// (inside-out order, tile_row) start while frame z's longest waves still run:
+// one tail per batch instead of one per frame.  Production builds only.
+#ifndef RM_KERNELS_AA_ONLY
+__global__ __launch_bounds__(64, 8) void k_pixel_frames(FrameBatch B) {
+  pixel_body<false>(B.f[blockIdx.z]);
+}
+#endif
+#ifndef RM_KERNELS_PIXEL_ONLY
+__global__ __launch_bounds__(64, 8) void k_sample_frames(FrameBatch B) {
+  sample_body<false>(B.f[blockIdx.z]);
+}
+#endif
+
+// Reassemble packed shard images into the frame: shard r's rows start at row
+// r * rank_stride of `gathered` (rank_stride = rows_cap for [nshards][rows_cap]
+// [width]; n * rows_cap for one frame of a batch gathered as [nshards][n]
+// [rows_cap][width]).  One grid row per frame row: the source row (shard, local
+// row) is computed once per workgroup in scalar registers; lanes copy 16 B (4
+// pixels) each when rows are 16-B aligned (width % 4 == 0 and both images 16-B
+// aligned), one pixel otherwise.
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
                                                  int height, int row_block, int nshards,
-                                                 int rows_cap) {
+                                                 size_t rank_stride) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   for (int y = blockIdx.y; y < height; y += gridDim.y) {  // gridDim.y <= 65535
     const int b = y / row_block;
     const int r = b % nshards;
     const int lrow = (b / nshards) * row_block + y % row_block;
-    const uint32_t* src = gathered + ((size_t)r * rows_cap + lrow) * (size_t)width;
+    const uint32_t* src = gathered + ((size_t)r * rank_stride + lrow) * (size_t)width;
     uint32_t* dst = frame + (size_t)y * (size_t)width;
     if (VEC) {
       if (i < width / 4)
@@ -583,7 +600,25 @@ hipError_t launch_sample(const rmd::Frame& F, bool counters, hipStream_t s) {
   return hipGetLastError();
 }
 #endif
+#ifndef RM_KERNELS_PIXEL_ONLY
+// n frames of one size and AA setting (rm_dispatch_frames): B.f[0..n) are set,
+// every frame's grid_x / grid_y equal to the first's
+hipError_t launch_sample_frames(const rmd::FrameBatch& B, int n, hipStream_t s) {
+  const dim3 grid(B.f[0].grid_x, B.f[0].grid_y, n);
+  hipLaunchKernelGGL(rmd::k_sample_frames, grid, dim3(64), 0, s, B);
+  return hipGetLastError();
+}
+#endif
 #ifndef RM_KERNELS_AA_ONLY
+hipError_t launch_sample_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
+hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s) {
+  if (n < 1 || n > rmd::kMaxBatch) return hipErrorInvalidValue;
+  if (B.f[0].aa) return launch_sample_frames(B, n, s);
+  const dim3 grid(B.f[0].grid_x, B.f[0].grid_y, n);
+  hipLaunchKernelGGL(rmd::k_pixel_frames, grid, dim3(64), 0, s, B);
+  return hipGetLastError();
+}
+
 hipError_t launch_sample(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s) {
   if (F.aa) return launch_sample(F, counters, s);
@@ -610,7 +645,8 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 
 #ifndef RM_KERNELS_AA_ONLY
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int nshards, int rows_cap, hipStream_t s) {
+                          int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows) {
+  const size_t stride = rank_stride_rows ? rank_stride_rows : (size_t)rows_cap;
   // 16-B copies need 16-B rows (width % 4 == 0) and 16-B aligned images: the
   // C-ABI takes caller pointers, which may be offset
   const bool vec = width % 4 == 0 && ((reinterpret_cast<uintptr_t>(gathered) |
@@ -621,10 +657,10 @@ hipError_t launch_unshard(const void* gathered, void* frame, int width, int heig
   uint32_t* f = static_cast<uint32_t*>(frame);
   if (vec)
     hipLaunchKernelGGL(rmd::k_unshard<true>, grid, dim3(256), 0, s, g, f, width, height, row_block,
-                       nshards, rows_cap);
+                       nshards, stride);
   else
     hipLaunchKernelGGL(rmd::k_unshard<false>, grid, dim3(256), 0, s, g, f, width, height, row_block,
-                       nshards, rows_cap);
+                       nshards, stride);
   return hipGetLastError();
 }
 #endif

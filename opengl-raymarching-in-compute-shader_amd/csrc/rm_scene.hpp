@@ -101,6 +101,16 @@ struct Frame {
                            // arguments, loaded with the rest of the prologue's
 };
 
+// A batch of frames of one context (rm_dispatch_frames): one grid over n frames
+// of the same size and AA setting, frame z = blockIdx.z, each with its own
+// constants and output pointers.  Kernel arguments, like a single Frame: the
+// frame's fields are scalar loads from the kernarg segment at a wave-uniform
+// offset.
+constexpr int kMaxBatch = 32;  // == RM_MAX_BATCH (rm_api.h; static_assert in rm_api.hip)
+struct FrameBatch {
+  Frame f[kMaxBatch];
+};
+
 // ---- scene: computeShader.glsl:83-123 ----------------------------------------
 // Three exact evaluations of the same sdf (value and opU id equal to a literal
 // transcription):

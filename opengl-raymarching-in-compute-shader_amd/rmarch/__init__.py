@@ -32,6 +32,10 @@ RM_ERR_NO_DEVICE = -4
 RM_ERR_STATE = -5
 RM_ERR_COMM = -6
 
+RM_API_VERSION = 4
+RM_CONFIG_MAGIC = 0x34434D52
+
+RM_MAX_BATCH = 32
 RM_OUT_RGBA8 = 1
 RM_OUT_RGBA32F = 2
 RM_SHADOW_SOFT = 0
@@ -75,7 +79,7 @@ class rm_counters(C.Structure):
 
 
 class rm_config(C.Structure):
-    _fields_ = [("struct_size", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
+    _fields_ = [("struct_size", C.c_uint32), ("magic", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
                 ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
                 ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32),
                 ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
@@ -160,6 +164,9 @@ _SIGS = {
     "rm_get_uniforms": (C.c_int, [_P, C.POINTER(rm_uniforms)]),
     "rm_default_uniforms": (C.c_int, [C.POINTER(rm_uniforms)]),
     "rm_dispatch": (C.c_int, [_P]),
+    "rm_dispatch_frames": (C.c_int, [_P, C.POINTER(rm_uniforms), C.c_int32]),
+    "rm_read_frame_rgba8": (C.c_int, [_P, C.c_int32, _P, C.c_size_t, C.c_int]),
+    "rm_read_frame_rgba32f": (C.c_int, [_P, C.c_int32, _P, C.c_size_t, C.c_int]),
     "rm_synchronize": (C.c_int, [_P]),
     "rm_read_rgba8": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
     "rm_read_rgba32f": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
@@ -207,6 +214,8 @@ _SIGS = {
     "rm_comm_init": (C.c_int, [_P, C.c_void_p, C.c_int32, C.c_int32]),
     "rm_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                C.POINTER(C.c_int32)]),
+    "rm_comm_rccl_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rm_comm_set_timeout": (C.c_int, [_P, C.c_int32]),
     "rm_comm_check": (C.c_int, [_P]),
 }
@@ -387,7 +396,7 @@ class Renderer:
         devs = (C.c_int32 * len(devices))(*devices) if devices else None
         if devices:
             ngpus = len(devices)
-        cfg = rm_config(struct_size=C.sizeof(rm_config), width=width, height=height,
+        cfg = rm_config(struct_size=C.sizeof(rm_config), magic=RM_CONFIG_MAGIC, width=width, height=height,
                         device=device, outputs=outputs, kernel=kernel,
                         counters=1 if counters else 0, row_block=row_block, shard=shard,
                         nshards=nshards, ngpus=ngpus,
@@ -493,6 +502,24 @@ class Renderer:
             self.set_uniforms(u)
         _check(lib().rm_dispatch(self._h), self._h)
 
+    def dispatch_frames(self, frames: Sequence[rm_uniforms]) -> None:
+        """Render len(frames) frames in one launch (rm_dispatch_frames): the images of
+        set_uniforms + dispatch per frame; afterwards the image is the last frame's and
+        read_frame_rgba8(k) reads frame k.  Asynchronous."""
+        n = len(frames)
+        arr = (rm_uniforms * n)(*frames)
+        _check(lib().rm_dispatch_frames(self._h, arr, n), self._h)
+
+    def read_frame_rgba8(self, k: int, flip_y: bool = False) -> np.ndarray:
+        out = np.empty((self.rows, self.width, 4), np.uint8)
+        _check(lib().rm_read_frame_rgba8(self._h, k, out.ctypes.data, 0, int(flip_y)), self._h)
+        return out
+
+    def read_frame_rgba32f(self, k: int, flip_y: bool = False) -> np.ndarray:
+        out = np.empty((self.rows, self.width, 4), np.float32)
+        _check(lib().rm_read_frame_rgba32f(self._h, k, out.ctypes.data, 0, int(flip_y)), self._h)
+        return out
+
     def graph_enable(self, on: bool = True) -> None:
         """Switch to hipGraph replay of the frame (BASELINE cfg 5)."""
         _check(lib().rm_graph_enable(self._h, int(on)), self._h)
@@ -569,6 +596,14 @@ class Renderer:
         r, n, g = C.c_int32(0), C.c_int32(0), C.c_int32(0)
         _check(lib().rm_comm_info(self._h, C.byref(r), C.byref(n), C.byref(g)), self._h)
         return r.value, n.value, g.value
+
+    def rccl_info(self) -> dict:
+        """What RCCL itself reports for this context's communicator (rm_comm_rccl_info):
+        ncclCommCount, ncclCommUserRank, ncclCommCuDevice, ncclGetVersion."""
+        n, r, d, v = C.c_int32(0), C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        _check(lib().rm_comm_rccl_info(self._h, C.byref(n), C.byref(r), C.byref(d), C.byref(v)),
+               self._h)
+        return {"count": n.value, "user_rank": r.value, "hip_device": d.value, "version": v.value}
 
     def enable_timing(self, on: bool = True) -> None:
         _check(lib().rm_enable_timing(self._h, int(on)), self._h)

@@ -44,7 +44,7 @@ def test_structs_match_header_sizes(rm):
     assert C.sizeof(rm.rm_light) == 60
     assert C.sizeof(rm.rm_uniforms) == 64 + 60 + 4 * 5 + 12 + 8 + 4
     assert C.sizeof(rm.rm_counters) == 56
-    assert C.sizeof(rm.rm_config) == 56  # struct_size + 10 int32 (+4 pad) + the devices pointer
+    assert C.sizeof(rm.rm_config) == 56  # struct_size + magic + 10 int32 + the devices pointer
     assert C.sizeof(rm.rm_camera_state) == 8 + 24 + 48
 
 
@@ -74,7 +74,7 @@ def test_struct_layouts_match_the_c_compiler(rm, tmp_path):
 
 
 def test_api_version(rm):
-    assert rm.lib().rm_api_version() == 3
+    assert rm.lib().rm_api_version() == 4 == rm.RM_API_VERSION
 
 
 def test_config_struct_size_is_checked(rm):
@@ -83,12 +83,18 @@ def test_config_struct_size_is_checked(rm):
     refuses it before reading any later field."""
     cfg = rm.rm_config()
     assert rm.lib().rm_config_init(C.byref(cfg), 64, 32) == 0
-    assert (cfg.struct_size, cfg.width, cfg.height, cfg.device, cfg.outputs, cfg.nshards,
-            cfg.ngpus) == (C.sizeof(rm.rm_config), 64, 32, -1, rm.RM_OUT_RGBA8, 1, 0)
-    old = rm.rm_config(struct_size=3840, width=2160, height=-1)  # a v1/v2 layout read as v3
+    assert (cfg.struct_size, cfg.magic, cfg.width, cfg.height, cfg.device, cfg.outputs, cfg.nshards,
+            cfg.ngpus) == (C.sizeof(rm.rm_config), rm.RM_CONFIG_MAGIC, 64, 32, -1, rm.RM_OUT_RGBA8, 1, 0)
+    old = rm.rm_config(struct_size=3840, magic=2160)  # a v1/v2 layout (width, height) read as v4
     h = C.c_void_p()
     assert rm.lib().rm_create(C.byref(h), C.byref(old)) == rm.RM_ERR_INVALID
     assert b"struct_size" in rm.lib().rm_last_error(None)
+    assert not h.value
+    # ADVICE r03: a v3 host's struct has the same size (56 on LP64) and its second
+    # word is the width: the magic refuses it
+    v3 = rm.rm_config(struct_size=C.sizeof(rm.rm_config), magic=1920, width=1080)
+    assert rm.lib().rm_create(C.byref(h), C.byref(v3)) == rm.RM_ERR_INVALID
+    assert b"magic" in rm.lib().rm_last_error(None)
     assert not h.value
 
 

@@ -1,0 +1,215 @@
+"""Frame batches (rm_dispatch_frames, API version 4): n frames in one launch.
+
+A batch must produce, for every frame k, exactly the image that
+rm_set_uniforms(frames[k]) + rm_dispatch (glDispatchCompute, main.cpp:123)
+produces: the batched kernels (k_pixel_frames / k_sample_frames, grid.z = the
+frame) are separate code objects from k_pixel / k_sample, so every test here
+compares them byte for byte (RGBA8) and bit for bit (RGBA32F) with the
+per-frame kernels, whose parity with the oracle the other suites pin, and the
+small-frame test also checks a batch against the oracle directly.  Afterwards
+the context must read as after n rm_dispatch calls (its image = the last frame,
+its uniforms = the last frame's).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(rm, n, b=3, aa=True, shadow=0):
+    return [rm.sweep_uniforms(int(f), 120, b, aa, shadow) for f in np.linspace(0, 119, n).astype(int)]
+
+
+def _per_frame(rm, W, H, us, outputs=None, **kw):
+    outputs = outputs or (rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F)
+    with rm.Renderer(W, H, outputs=outputs, **kw) as r:
+        out = []
+        for u in us:
+            r.dispatch(u)
+            out.append((r.read_rgba8() if outputs & rm.RM_OUT_RGBA8 else None,
+                        r.read_rgba32f() if outputs & rm.RM_OUT_RGBA32F else None))
+        return out
+
+
+def _check_batch(rm, r, us, ref):
+    for k, (w8, w32) in enumerate(ref):
+        if w8 is not None:
+            np.testing.assert_array_equal(r.read_frame_rgba8(k), w8, err_msg=f"frame {k}")
+        if w32 is not None:
+            np.testing.assert_array_equal(r.read_frame_rgba32f(k).view(np.uint32), w32.view(np.uint32),
+                                          err_msg=f"frame {k} (RGBA32F)")
+    # the context reads as after len(us) dispatches
+    if ref[-1][0] is not None:
+        np.testing.assert_array_equal(r.read_rgba8(), ref[-1][0])
+    u = r.get_uniforms()
+    assert bytes(u) == bytes(us[-1])
+
+
+@pytest.mark.parametrize("W,H,b,aa,shadow,n", [
+    (160, 90, 3, True, 0, 7),     # cfg3-like, supersampled
+    (192, 108, 1, False, 0, 12),  # cfg2-like
+    (64, 64, 0, False, 1, 32),    # cfg1-like (hard shadows), the largest batch
+    (37, 23, 5, True, 0, 3),      # ragged tiles, 5 bounces
+    (1, 1, 2, False, 0, 2),
+])
+def test_batch_equals_per_frame_dispatch(rm, gpu, W, H, b, aa, shadow, n):
+    us = _frames(rm, n, b, aa, shadow)
+    ref = _per_frame(rm, W, H, us)
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
+        r.dispatch_frames(us)
+        _check_batch(rm, r, us, ref)
+        # a second, shorter batch and a plain dispatch reuse the ring
+        r.dispatch_frames(us[:2])
+        _check_batch(rm, r, us[:2], ref[:2])
+        r.dispatch(us[-1])
+        np.testing.assert_array_equal(r.read_frame_rgba8(0), ref[-1][0])
+        with pytest.raises(rm.RMError):
+            r.read_frame_rgba8(1)  # a plain dispatch holds one frame
+
+
+def test_batch_matches_oracle(rm, gpu, oracle):
+    """The batched kernels against the CPU oracle directly (geometry exact, RGBA8 <= 1 LSB)."""
+    W, H = 96, 54
+    us = _frames(rm, 4, 3, True) + _frames(rm, 3, 1, False)  # two AA runs: two launches
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8) as r:
+        r.dispatch_frames(us)
+        for k, u in enumerate(us):
+            ref = oracle.render(u, W, H)
+            d = np.abs(r.read_frame_rgba8(k).astype(np.int16) - ref["rgba8"].astype(np.int16))
+            assert d.max() <= 1, (k, int(d.max()))
+
+
+def test_batch_mixed_uniforms(rm, gpu):
+    """Every uniform may change inside a batch (bounces, AA, shadow mode, light)."""
+    W, H = 128, 72
+    us = [rm.sweep_uniforms(f, 120, f % 6, f % 3 == 0, f % 2) for f in range(0, 120, 7)]
+    us[3].light.position[1] = -3.0
+    us[5].iTime = 123.0
+    ref = _per_frame(rm, W, H, us)
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
+        r.dispatch_frames(us)
+        _check_batch(rm, r, us, ref)
+
+
+def test_batch_sharded_and_external_output(rm, gpu):
+    import torch
+    W, H = 160, 90
+    us = _frames(rm, 5)
+    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8, row_block=8, shard=1, nshards=3)
+    with rm.Renderer(W, H, row_block=8, shard=1, nshards=3) as r:
+        r.dispatch_frames(us)
+        _check_batch(rm, r, us, ref)
+        out = torch.zeros((r.rows, W, 4), dtype=torch.uint8, device="cuda")
+        r.set_output_rgba8(out.data_ptr())
+        r.dispatch_frames(us)
+        r.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), ref[-1][0])  # the last frame lands there
+        np.testing.assert_array_equal(r.read_frame_rgba8(1), ref[1][0])
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_batch_scene_table(rm, gpu, spec):
+    """A runtime scene table renders a batch one launch per frame: same images."""
+    W, H = 128, 72
+    us = _frames(rm, 4)
+    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
+    with rm.Renderer(W, H) as r:
+        if spec:
+            r.specialize_scene(True)
+        r.set_scene(rm.default_scene())
+        r.dispatch_frames(us)
+        _check_batch(rm, r, us, ref)
+
+
+@pytest.mark.parametrize("form", ["comm_init", "ngpus"])
+def test_batch_on_communicator_contexts(rm, gpu, form):
+    """One rank (rm_comm_init) / one device (rm_config.ngpus): the batch's shards move
+    in one ncclGather on the gather stream and rank 0 assembles every frame; plain
+    dispatches and graph replays interleave with batches in order."""
+    W, H, R = 160, 90, 8
+    us = _frames(rm, 9)
+    ref = _per_frame(rm, W, H, us)
+    outs = rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F
+    if form == "ngpus":
+        r = rm.Renderer(W, H, outputs=outs, ngpus=1, row_block=R)
+    else:
+        r = rm.Renderer(W, H, outputs=outs, row_block=R, shard=0, nshards=1)
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+    with r:
+        for rep in range(3):  # both slots, then the first again
+            r.dispatch_frames(us)
+            _check_batch(rm, r, us, ref)
+        # batches back to back without a read between them (slot reuse ordering)
+        r.dispatch_frames(us[:4])
+        r.dispatch_frames(us[4:])
+        _check_batch(rm, r, us[4:], ref[4:])
+        r.dispatch(us[2])
+        np.testing.assert_array_equal(r.read_rgba8(), ref[2][0])
+        r.dispatch_frames(us[:3])
+        r.dispatch(us[7])  # ordered after the batch's gather
+        np.testing.assert_array_equal(r.read_rgba8(), ref[7][0])
+        r.graph_enable(True)
+        r.graph_dispatch(us[5])
+        r.graph_dispatch(us[6])
+        np.testing.assert_array_equal(r.read_rgba8(), ref[6][0])
+        r.dispatch_frames(us[:2])
+        _check_batch(rm, r, us[:2], ref[:2])
+
+
+def test_batch_timing_and_phases(rm, gpu):
+    W, H = 160, 90
+    us = _frames(rm, 6)
+    with rm.Renderer(W, H, row_block=8, shard=0, nshards=1) as r:
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+        r.enable_timing(True)
+        r.kernel_time_ms(reset=True)
+        r.dispatch_frames(us)
+        ms, n = r.kernel_time_ms(reset=True)
+        assert n == 6 and ms > 0  # a batch counts its frames
+        ph = r.frame_phases()
+        assert ph["render_ms"] > 0 and ph["gather_ms"] >= 0 and ph["assemble_ms"] > 0
+
+
+def test_batch_validation(rm, gpu):
+    us = _frames(rm, 2)
+    with rm.Renderer(32, 32) as r:
+        for bad in ([], us * 17):  # n = 0, n = 34 > RM_MAX_BATCH
+            with pytest.raises(rm.RMError) as e:
+                if bad:
+                    r.dispatch_frames(bad)
+                else:
+                    import ctypes as C
+                    rm._check(rm.lib().rm_dispatch_frames(r.handle, (rm.rm_uniforms * 1)(), 0), r.handle)
+            assert e.value.code == rm.RM_ERR_INVALID
+        bad = _frames(rm, 2)
+        bad[1].bounceVar = 6
+        with pytest.raises(rm.RMError) as e:
+            r.dispatch_frames(bad)
+        assert e.value.code == rm.RM_ERR_INVALID
+        with pytest.raises(rm.RMError) as e:
+            r.read_frame_rgba8(0)  # nothing dispatched yet
+        assert e.value.code == rm.RM_ERR_STATE
+        r.dispatch_frames(us)
+        for k in (-1, 2):
+            with pytest.raises(rm.RMError) as e:
+                r.read_frame_rgba8(k)
+            assert e.value.code == rm.RM_ERR_INVALID
+    with rm.Renderer(32, 32, counters=True) as r:
+        with pytest.raises(rm.RMError) as e:
+            r.dispatch_frames(us)
+        assert e.value.code == rm.RM_ERR_STATE
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_batch_full_size(rm, gpu, cfg):
+    """BASELINE cfg2 / cfg3 at full size: a 20-frame batch of the bench's sweep frames
+    equals the per-frame production kernel on every pixel of every frame."""
+    W, H, b, aa = {2: (1920, 1080, 1, False), 3: (3840, 2160, 3, True)}[cfg]
+    frames = [(k * 120) // 20 for k in range(20)]
+    us = [rm.sweep_uniforms(f, 120, b, aa, 0) for f in frames]
+    with rm.Renderer(W, H) as r, rm.Renderer(W, H) as one:
+        r.dispatch_frames(us)
+        r.synchronize()
+        for k, u in enumerate(us):
+            one.dispatch(u)
+            np.testing.assert_array_equal(r.read_frame_rgba8(k), one.read_rgba8(), err_msg=f"frame {frames[k]}")

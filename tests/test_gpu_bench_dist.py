@@ -32,6 +32,9 @@ def _free_port():
     ("--config", "2", "--steps", "4", "--warmup", "2"),
     ("--config", "3", "--steps", "3", "--warmup", "1", "--pipeline", "0"),
     ("--config", "2", "--steps", "5", "--warmup", "2", "--graph", "1"),
+    # one communicator per rank: batches of frames gathered on the context's gather stream
+    ("--config", "2", "--steps", "9", "--warmup", "2", "--comms", "1", "--batch", "4"),
+    ("--config", "3", "--steps", "4", "--warmup", "1", "--comms", "1", "--batch", "2"),
 ])
 def test_bench_rccl_path_at_world_size_one(args):
     """bench.py's N > 1 step with its real RCCL calls (librm communicators, gather
@@ -48,8 +51,18 @@ def test_bench_rccl_path_at_world_size_one(args):
     assert d["n_gpus"] == 1 and "RCCL gather" in d["config"]["parallelism"]
     p = d["parity"]
     assert p["assembled_equals_single_gpu"] and p["max_abs_delta_rgba8"] == 0, p
-    ph = d["phases"]  # per-rank render / gather / assembly split
-    assert len(ph["per_rank"]) == 1 and ph["max_render_ms"] > 0 and ph["assemble_ms"] > 0, ph
+    # per-rank render / gather / assembly split over every timed frame
+    ph = d["phases"]
+    steps = int(args[args.index("--steps") + 1])
+    assert len(ph["per_rank"]) == 1 and ph["frames"] == steps, ph
+    assert ph["max_render_mean_ms"] > 0 and ph["max_render_max_ms"] >= ph["max_render_mean_ms"], ph
+    assert ph["assemble_mean_ms"] > 0 and ph["max_gather_max_ms"] >= ph["max_gather_mean_ms"] >= 0, ph
+    # what RCCL itself formed: every communicator of every rank is rank r of WORLD_SIZE
+    rc = d["rccl"]
+    assert rc["nranks_seen"] == [1] and rc["all_communicators_match"] and rc["version"] > 0, rc
+    ncomm = d["config"]["communicators_per_rank"]
+    one = "--comms" in args or ("--pipeline" in args and args[args.index("--pipeline") + 1] == "0")
+    assert len(rc["per_rank"][0]["comms"]) == ncomm == (1 if one else 4), rc
     assert "render kernel" in d["roofline"]["kernel_time_basis"] or args[-1] == "0"
 
 

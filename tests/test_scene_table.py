@@ -7,6 +7,7 @@ literal transcription of sdf() bit for bit — colours, NaN masks and work count
 which pins the table semantics (entry order, swizzle, blend, checkers paint, ids,
 materials) to the reference scene.  No GPU calls."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -135,3 +136,55 @@ def test_table_specialises_without_a_device(rm):
     bad = rm.default_scene()
     bad[0].type = 9
     assert _code_object(rm, bad)[0] == rm.RM_ERR_INVALID
+
+
+def test_table_compiles_once(rm, tmp_path):
+    """rm_scene_specialize compiles the reference scene's table once.
+    The unbounded build's kernel descriptors give the production kernels' VGPR
+    allocation (72: 7 waves per SIMD, no scratch), so no occupancy ladder runs; the
+    hiprtc invocations are counted from RM_JIT_LOG's one line per compile."""
+    import subprocess
+    import sys
+    prog = (
+        "import ctypes as C, sys\n"
+        f"sys.path.insert(0, {os.path.dirname(rm.__file__)!r}.rsplit('/', 1)[0])\n"
+        "import rmarch as rm\n"
+        "sc = rm.default_scene()\n"
+        "tbl = (rm.rm_primitive * len(sc))(*sc)\n"
+        "size = C.c_size_t(0)\n"
+        "assert rm.lib().rm_jit_code_object(tbl, len(sc), b'gfx950', None, 0, C.byref(size)) == 0\n"
+        "assert size.value > 0\n")
+    out = subprocess.run([sys.executable, "-c", prog], env=dict(os.environ, RM_JIT_LOG="1"),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [x for x in out.stderr.splitlines() if x.startswith("rm_jit: hiprtc compile")]
+    assert len(lines) == 1, out.stderr
+    rc, co = _code_object(rm, rm.default_scene())
+    assert rc == 0
+    vg = _kernel_vgprs(co)
+    prod = {k: v for k, v in vg.items() if "ILb0E" in k}
+    assert len(prod) == 2 and all(v <= 72 for v in prod.values()), vg  # >= 7 waves per SIMD
+
+
+def _kernel_vgprs(co):
+    """VGPR allocation per lane of every kernel (compute_pgm_rsrc1 bits 5:0 of its
+    descriptor at offset 48: allocation / 8 - 1 on gfx950)."""
+    import struct
+    shoff, = struct.unpack_from("<Q", co, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", co, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", co, shoff + i * shentsize) for i in range(shnum)]
+    out = {}
+    for name_, type_, flags, addr, off, size, link, info, align, entsize in secs:
+        if type_ != 2:
+            continue
+        stroff = secs[link][4]
+        for k in range(size // 24):
+            st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
+                "<IBBHQQ", co, off + 24 * k)
+            end = co.index(b"\0", stroff + st_name)
+            sym = co[stroff + st_name:end].decode()
+            if sym.endswith(".kd") and st_shndx < shnum:
+                sec = secs[st_shndx]
+                kd = sec[4] + (st_value - sec[3])
+                out[sym[:-3]] = ((struct.unpack_from("<I", co, kd + 48)[0] & 0x3F) + 1) * 8
+    return out

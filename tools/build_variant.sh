@@ -22,11 +22,12 @@ flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-c
 b=$(mktemp -d)
 /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_api.hip" -o "$b/rm_api.o" &
 /opt/rocm/bin/hipcc $flags -fno-slp-vectorize -c "$src/$pkg/csrc/rm_table.hip" -o "$b/rm_table.o" &
-# rm_kernels.hip as the Makefile builds it (k_sample alone, without SLP), except
+# rm_kernels.hip as the Makefile builds it (both objects without SLP; RM_PIXEL_SLP=1
+# builds k_pixel with it, the round-3 flags), except
 # for the RM_STATS build, whose counters must live in one code object
 case "$*" in
   *RM_STATS*) /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" & ;;
-  *) /opt/rocm/bin/hipcc $flags -O2 -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
+  *) /opt/rocm/bin/hipcc $flags -O2 ${RM_PIXEL_SLP:+-fslp-vectorize} ${RM_PIXEL_SLP:--fno-slp-vectorize} -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
      /opt/rocm/bin/hipcc $flags -O2 -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels_aa.o" & ;;
 esac
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &

@@ -1,9 +1,13 @@
 """Render the bench's sweep frames with one kernel variant (driver for rocprofv3 --pmc).
 
-  python tools/prof_kernels.py KIND CFG STEPS
+  python tools/prof_kernels.py KIND CFG STEPS [BATCH]
 KIND: pixel | table | table-spec.  The frames are bench.py's own
 (bench_frames(STEPS): step k renders sweep frame floor(k * 120 / STEPS)), one
-launch each, so the per-launch PMC means describe the benched workload.
+launch each, so the per-launch PMC means describe the benched workload.  BATCH >
+1 (pixel only): the same frames once more as rm_dispatch_frames batches of
+BATCH frames (k_pixel_frames / k_sample_frames, the kernels bench.py times for
+that configuration); tools/summarize_profiles.py divides their per-launch
+counters by BATCH.
 """
 import os
 import sys
@@ -17,13 +21,19 @@ from bench import CONFIGS, bench_frames  # noqa: E402
 kname = sys.argv[1] if len(sys.argv) > 1 else "pixel"
 cfg = CONFIGS[int(sys.argv[2]) if len(sys.argv) > 2 else 3]
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 k = rm.RM_KERNEL_PIXEL
 with rm.Renderer(cfg["width"], cfg["height"], kernel=k) as r:
     if kname == "table-spec":  # the same, with kernels compiled for the table (hiprtc)
         r.specialize_scene(True)
     if kname in ("table", "table-spec"):  # the reference scene as a runtime table (k_table_* kernels)
         r.set_scene(rm.default_scene())
-    for f in bench_frames(steps):
-        r.dispatch(rm.sweep_uniforms(f, 120, cfg["bounces"], cfg["aa"], cfg["shadow"]))
+    us = [rm.sweep_uniforms(f, 120, cfg["bounces"], cfg["aa"], cfg["shadow"]) for f in bench_frames(steps)]
+    for u in us:
+        r.dispatch(u)
     r.synchronize()
+    if batch > 1 and kname == "pixel":
+        for i in range(0, len(us), batch):
+            r.dispatch_frames(us[i:i + batch])
+        r.synchronize()
 print("done", kname, sys.argv[2:])
