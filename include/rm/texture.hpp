@@ -61,6 +61,11 @@ inline int setVec4(rm_ctx* p, const std::string& n, float x, float y, float z, f
 }
 // main.cpp:123 / :125
 inline int dispatchCompute(rm_ctx* p) { return rm_dispatch(p); }
+// n frames of uniforms in one launch (rm_dispatch_frames, API version 4): the
+// images of n dispatchCompute calls; frame k via rm_read_frame_rgba8(p, k, ...)
+inline int dispatchFrames(rm_ctx* p, const rm_uniforms* frames, int n) {
+  return rm_dispatch_frames(p, frames, n);
+}
 inline int memoryBarrier(rm_ctx* p) { return rm_synchronize(p); }
 
 }  // namespace rm

@@ -309,6 +309,10 @@ int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
  * gather) into `frame` ([height][width] RGBA8), both device pointers, on the
  * context's stream. Uses the context's width/height/row_block/nshards. */
 int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
+/* The same for frame k of an n-frame batch gathered as rm_dispatch_frames
+ * gathers it: [nshards][n][rows_cap][width] RGBA8 (each rank's n shards back to
+ * back, ranks in order), e.g. by a host that moves the shards itself. */
+int rm_unshard_batch_rgba8(rm_ctx *ctx, const void *gathered_dev, int32_t k, int32_t n, void *frame_dev);
 /* Kernel timing: when enabled, HIP events bracket every render-kernel launch
  * on the launch stream; rm_kernel_time_ms returns the summed kernel time and
  * launch count since the last reset (synchronizes). */

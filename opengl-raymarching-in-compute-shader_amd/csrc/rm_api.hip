@@ -468,6 +468,9 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.blend = std::sin(u.iTime) / 2.0f + 0.5f;
   F.omblend = 1.0f - F.blend;
   F.k = (u.shadow_mode == RM_SHADOW_HARD) ? INFINITY : 2.0f;
+  // the soft-shadow exit's ratio bound (rm_scene.hpp shadow_exit_init), the
+  // device's former per-call expression in the same float operations
+  F.shc = (F.k == INFINITY) ? 0.0f : (1.0f + 0x1p-9f) / F.k * (1.0f + 0x1p-12f);
   F.persp = 45.0f * static_cast<float>(0.01745329251994329576923690768489);
   F.uvx = c->d_uv;
   F.uvy = c->d_uv + (size_t)5 * c->cfg.width;
@@ -1766,6 +1769,20 @@ int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
   if (rc != RM_OK) return rc;
   hipError_t e = rm::launch_unshard(gathered_dev, frame_dev, c->cfg.width, c->cfg.height,
                                     c->cfg.row_block, c->cfg.nshards, c->rows, c->stream);
+  if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
+  return RM_OK;
+}
+
+int rm_unshard_batch_rgba8(rm_ctx* c, const void* gathered_dev, int32_t k, int32_t n, void* frame_dev) {
+  if (!c || !gathered_dev || !frame_dev) return RM_ERR_INVALID;
+  if (n < 1 || k < 0 || k >= n) return fail(c, RM_ERR_INVALID, "rm_unshard_batch_rgba8: need 0 <= k < n");
+  if (!c->subs.empty()) return fail(c, RM_ERR_STATE, "a multi-GPU context assembles its own frames");
+  int rc = set_device(c);
+  if (rc != RM_OK) return rc;
+  const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
+  const uint8_t* src = static_cast<const uint8_t*>(gathered_dev) + (size_t)k * px * 4;
+  hipError_t e = rm::launch_unshard(src, frame_dev, c->cfg.width, c->cfg.height, c->cfg.row_block,
+                                    c->cfg.nshards, c->rows, c->stream, (size_t)n * (size_t)c->rows);
   if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }

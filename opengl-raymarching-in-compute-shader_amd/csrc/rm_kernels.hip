@@ -283,7 +283,7 @@ __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, C
   float res = 1.0f, t = 0.0f;
   int dummy;
   RM_STAT(29);
-  const float ex = shadow_exit_init(F.k, ro, rd);
+  const float ex = shadow_exit_init(F.shc, ro, rd);
   for (int i = 0; i < 16; ++i) {
     if (lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;

@@ -71,6 +71,8 @@ struct Frame {
   float blend;     // sin(iTime)/2 + 0.5, host sinf (glsl:117)
   float omblend;   // 1 - blend (uniform-only subexpression of mix)
   float k;         // softshadow k: 2.0 (glsl:185,236) or +inf (hard-shadow extension)
+  float shc;       // the soft-shadow exit's ratio bound c = (1 + 2^-9) / k (1 + 2^-12), 0 for
+                   // k = +inf (shadow_exit_init): uniform, formed once per frame on the host
   float persp;     // radians(45) = 45 * 0.017453292519943295f (glsl:70)
   // uv of every pixel column / row, host IEEE in the shader's order (glsl:301-332):
   // [k = 0] (2 p - dims) / dims, [k = 1 + s] after the cumulative sub-sample
@@ -657,8 +659,11 @@ __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd
   lin_exit_b(ro, s0, hmin, b1, b2);
   return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2);
 }
-__device__ __forceinline__ float shadow_exit_init(float k, f3 ro, f3 rd) {
-  const float c = (k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / k * (1.0f + 0x1p-12f);
+// c = Frame::shc, (1 + 2^-9) / k (1 + 2^-12) (0 for k = +inf): the host forms it
+// with the same float operations once per frame (rm_api.hip make_frame), where
+// the device would have spent a full IEEE division (~14 VALU) per shadow call
+// site and wave on a uniform value.
+__device__ __forceinline__ float shadow_exit_init(float c, f3 ro, f3 rd) {
   return lin_exit_init(c, 0.001f, ro, rd);
 }
 __device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd); }

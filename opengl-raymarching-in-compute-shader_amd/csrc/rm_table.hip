@@ -637,7 +637,7 @@ __device__ RM_TS_INLINE f3 tnormal(const Table& S, f3 pos, TCnt& c, bool have_c0
 template <bool COUNT, int KL>
 __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   float res = 1.0f, t = 0.0f;
-  const float c_sh = (F.k == __builtin_huge_valf()) ? 0.0f : (1.0f + 0x1p-9f) / F.k * (1.0f + 0x1p-12f);
+  const float c_sh = F.shc;  // (1 + 2^-9) / k (1 + 2^-12), 0 for k = +inf (host, make_frame)
   const float T = table_exit_T(S.exits(), c_sh, 0.001f, ro, rd);
   TLazy<KL> lz(S, ro, rd);
   for (int i = 0; i < 16; ++i) {

@@ -178,6 +178,7 @@ _SIGS = {
     "rm_set_output_rgba8": (C.c_int, [_P, _P]),
     "rm_get_output_rgba8": (C.c_int, [_P, C.POINTER(_P)]),
     "rm_unshard_rgba8": (C.c_int, [_P, _P, _P]),
+    "rm_unshard_batch_rgba8": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P]),
     "rm_enable_timing": (C.c_int, [_P, C.c_int]),
     "rm_kernel_time_ms": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]),
     "rm_frame_phases": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -568,6 +569,10 @@ class Renderer:
 
     def unshard_rgba8(self, gathered_ptr: int, frame_ptr: int) -> None:
         _check(lib().rm_unshard_rgba8(self._h, gathered_ptr, frame_ptr), self._h)
+
+    def unshard_batch_rgba8(self, gathered_ptr: int, k: int, n: int, frame_ptr: int) -> None:
+        """Frame k of an n-frame batch gathered as [nshards][n][rows_cap][width]."""
+        _check(lib().rm_unshard_batch_rgba8(self._h, gathered_ptr, k, n, frame_ptr), self._h)
 
     # -- one rank per process (rm_comm_init)
     def comm_init(self, comm_id: bytes, nranks: int, rank: int) -> None:

@@ -20,7 +20,10 @@
 //
 //   rm_frameloop [--width W] [--height H] [--frames N] [--bounces B] [--aa 0|1]
 //                [--hard-shadows] [--kernel auto|pixel] [--dump out.ppm]
-//                [--input script.txt] [--gpus N] [--graph]
+//                [--input script.txt] [--gpus N] [--graph] [--batch B]
+// --batch B renders B consecutive frames per launch (rm_dispatch_frames: the
+// setters run per frame as before, the uniforms of B frames are collected and
+// dispatched together; the last frame's image is the one dumped).
 #include <rm/camera.hpp>
 #include <rm/input.hpp>
 #include <rm/texture.hpp>
@@ -34,7 +37,7 @@
 
 int main(int argc, char** argv) {
   int W = 1080, H = 1080, frames = 120, bounce = 0, aa = 1, shadow = RM_SHADOW_SOFT;
-  int kernel = RM_KERNEL_AUTO, ngpus = 0, graph = 0;
+  int kernel = RM_KERNEL_AUTO, ngpus = 0, graph = 0, batch = 1;
   const char* dump = nullptr;
   const char* script = nullptr;
   for (int i = 1; i < argc; ++i) {
@@ -55,6 +58,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--input")) script = next("--input");
     else if (!std::strcmp(argv[i], "--gpus")) ngpus = std::atoi(next("--gpus"));
     else if (!std::strcmp(argv[i], "--graph")) graph = 1;
+    else if (!std::strcmp(argv[i], "--batch")) batch = std::atoi(next("--batch"));
     else if (!std::strcmp(argv[i], "--kernel")) {
       std::string k = next("--kernel");
       kernel = k == "pixel" ? RM_KERNEL_PIXEL : RM_KERNEL_AUTO;
@@ -62,6 +66,10 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "unknown flag %s\n", argv[i]);
       return 2;
     }
+  }
+  if (batch < 1 || batch > RM_MAX_BATCH || (batch > 1 && graph)) {
+    std::fprintf(stderr, "--batch must be in 1..%d (and not with --graph)\n", RM_MAX_BATCH);
+    return 2;
   }
   if (bounce < 0) bounce = 0;  // the key callback clamps to 0..5 (main.cpp:199-204)
   if (bounce > 5) bounce = 5;
@@ -94,6 +102,16 @@ int main(int argc, char** argv) {
     return 1;
   }
   unsigned int workgroups = 39;  // main.cpp:76-77 (ignored by librm)
+  std::vector<rm_uniforms> pending((size_t)batch);
+  int npending = 0;
+  auto flush = [&]() {
+    if (rm_dispatch_frames(marching, pending.data(), npending) != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
+      std::fprintf(stderr, "batch of %d frames failed: %s\n", npending, rm_last_error(marching));
+      return false;
+    }
+    npending = 0;
+    return true;
+  };
 
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -160,10 +178,15 @@ int main(int argc, char** argv) {
     rm::setVec2(marching, "iMouse", mu.iMouse[0], mu.iMouse[1]);
     rm::setInt(marching, "shadow_mode", shadow);
 
-    const int drc = graph ? rm_graph_dispatch(marching) : rm::dispatchCompute(marching);
-    if (drc != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
-      std::fprintf(stderr, "frame %d failed: %s\n", f, rm_last_error(marching));
-      return 1;
+    if (batch > 1) {  // collect this frame's uniforms; dispatch B frames at once
+      rm_get_uniforms(marching, &pending[npending++]);
+      if (npending == batch && !flush()) return 1;
+    } else {
+      const int drc = graph ? rm_graph_dispatch(marching) : rm::dispatchCompute(marching);
+      if (drc != RM_OK || rm::memoryBarrier(marching) != RM_OK) {
+        std::fprintf(stderr, "frame %d failed: %s\n", f, rm_last_error(marching));
+        return 1;
+      }
     }
     ++counter;
     ++total;
@@ -174,6 +197,7 @@ int main(int argc, char** argv) {
       counter = 0;
     }
   }
+  if (npending && !flush()) return 1;
   const double secs = std::chrono::duration<double>(clk::now() - t0).count();
   std::printf("frames %u  %.3f s  %.2f fps  %.2f Mpixels/s  (%dx%d, bounces %d, AA %d, gpus %d%s)\n",
               total, secs, total / secs, total * (double)W * H / secs / 1e6, W, H, bounce, aa,

@@ -213,3 +213,33 @@ def test_batch_full_size(rm, gpu, cfg):
         for k, u in enumerate(us):
             one.dispatch(u)
             np.testing.assert_array_equal(r.read_frame_rgba8(k), one.read_rgba8(), err_msg=f"frame {frames[k]}")
+
+
+@pytest.mark.parametrize("N,R,n", [(2, 8, 5), (3, 4, 3), (8, 8, 4)])
+def test_batch_gather_layout_assembles(rm, gpu, N, R, n):
+    """The N-rank layout of a gathered batch, rehearsed with N virtual ranks on one GPU
+    (RCCL refuses two ranks on one device): rank r's n shards rendered by
+    rm_dispatch_frames, placed as ncclGather places them on rank 0 ([N][n][rows_cap]
+    [width]: each rank's n shards back to back), and every frame k assembled by
+    rm_unshard_batch_rgba8 (the k_unshard launch rm_dispatch_frames uses on rank 0,
+    rank stride n x rows_cap) equals a full render."""
+    import torch
+    W, H = 160, 90
+    us = _frames(rm, n)
+    cap = rm.shard_rows_cap(H, R, N)
+    gathered = torch.zeros((N, n, cap, W, 4), dtype=torch.uint8, device="cuda")
+    for r in range(N):
+        with rm.Renderer(W, H, row_block=R, shard=r, nshards=N) as s:
+            s.dispatch_frames(us)
+            for k in range(n):
+                gathered[r, k] = torch.from_numpy(s.read_frame_rgba8(k)).cuda()
+    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
+    with rm.Renderer(W, H, row_block=R, shard=0, nshards=N) as a:
+        for k in range(n):
+            frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            a.unshard_batch_rgba8(gathered.data_ptr(), k, n, frame.data_ptr())
+            a.synchronize()
+            np.testing.assert_array_equal(frame.cpu().numpy(), ref[k][0], err_msg=f"frame {k}")
+        with pytest.raises(rm.RMError):
+            a.unshard_batch_rgba8(gathered.data_ptr(), n, n, frame.data_ptr())

@@ -88,6 +88,19 @@ def test_sweep_loop_last_frame(rm, oracle, gpu, tmp_path):
     np.testing.assert_array_equal(img, render(rm, W, H, rm.sweep_uniforms(F - 1, F, 2, True, rm.RM_SHADOW_SOFT)))
 
 
+@pytest.mark.parametrize("batch", [7, 32])
+def test_sweep_loop_batched(rm, oracle, gpu, tmp_path, batch):
+    """rm_frameloop --batch B: the same host loop, B frames per rm_dispatch_frames
+    (120 = 17 x 7 + 1 and 3 x 32 + 24: a short last batch); the dumped last frame
+    equals the per-frame loop's and the oracle's."""
+    W, H, F = 96, 64, 120
+    img, log = run_driver(tmp_path, "--width", W, "--height", H, "--frames", F,
+                          "--bounces", 2, "--aa", 1, "--batch", batch)
+    assert f"frames {F}" in log
+    assert_matches_oracle(oracle, img, golden_sweep_uniforms(rm, F - 1, 2, True), W, H)
+    np.testing.assert_array_equal(img, render(rm, W, H, rm.sweep_uniforms(F - 1, F, 2, True, rm.RM_SHADOW_SOFT)))
+
+
 def script_from_golden(events):
     lines = []
     for e in events:

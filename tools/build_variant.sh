@@ -27,7 +27,8 @@ b=$(mktemp -d)
 # for the RM_STATS build, whose counters must live in one code object
 case "$*" in
   *RM_STATS*) /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" & ;;
-  *) /opt/rocm/bin/hipcc $flags -O2 ${RM_PIXEL_SLP:+-fslp-vectorize} ${RM_PIXEL_SLP:--fno-slp-vectorize} -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
+  *) pslp=-fno-slp-vectorize; [ -n "$RM_PIXEL_SLP" ] && pslp=-fslp-vectorize
+     /opt/rocm/bin/hipcc $flags -O2 $pslp -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
      /opt/rocm/bin/hipcc $flags -O2 -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels_aa.o" & ;;
 esac
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
@@ -39,7 +40,7 @@ if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed t
     ../../include/rm_api.h=$src/include/rm_api.h
   /opt/rocm/bin/hipcc $flags -I"$b" -c "$c/rm_jit.hip" -o "$b/rm_jit.o" &
 fi
-wait
+for j in $(jobs -p); do wait "$j" || { echo "build_variant: a compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/librm_$name.so" "$b"/*.o -lhiprtc -ldl
 rm -rf "$b"; [ "$src" != "$root" ] && rm -rf "$src"
 echo "$out/librm_$name.so"
