@@ -333,11 +333,22 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
       if (COUNT) c.lights++;
       tcol = point_light(F, tcol, normal, pos);
     }
+    // The weights x / i (glsl:186-187).  For i = 1, 2, 4 the quotient is the
+    // real number x * 2^-k, exactly representable unless it underflows, and
+    // where it does the correctly rounded quotient and the correctly rounded
+    // product x * 2^-k round that same real number: x * (1, 0.5, 0.25) equals
+    // the IEEE division bit for bit.  i is wave-uniform, so this is a scalar
+    // branch, and 2 of cfg3's 3 bounce iterations skip four IEEE divisions
+    // (~10 VALU each) per lane.
+    const bool pow2 = (i & (i - 1)) == 0;
+    const float w = i == 1 ? 1.0f : (i == 2 ? 0.5f : 0.25f);
     if (id == 7 && !prevMatte && i < 3) {
       float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
-      color = muls(color, div_small(sh, i));
+      color = muls(color, pow2 ? sh * w : div_small(sh, i));
     }
-    color = add(color, divi(mul(tcol, prevColor), i));
+    const f3 tw = mul(tcol, prevColor);
+    if (pow2) color = add(color, muls(tw, w));
+    else color = add(color, divi(tw, i));
     prevColor = tcol;
     prevMatte = (id == 7);  // material of the hit: MATTE only for the floor; dummy is 1.0
   }

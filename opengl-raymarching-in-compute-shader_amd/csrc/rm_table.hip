@@ -688,14 +688,19 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
       if (COUNT) c.lights++;
       h.color = point_light(F, h.color, normal, pos);
     }
+    const bool pow2 = (i & (i - 1)) == 0;  // wave-uniform: a scalar branch
+    const float w = i == 1 ? 1.0f : (i == 2 ? 0.5f : 0.25f);
     if (h.id == 7 && i < 3) {  // prevObject.material != MATTE here
       float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
 #ifdef RM_TDBL_SHADOW
       if (!COUNT) sh = fminf(sh, tshadow<COUNT, KL>(F, S, topaque(add(pos, muls(normal, 0.02f))), sub(lpos, pos), c));
 #endif
-      color = muls(color, sh / (float)i);
+      color = muls(color, pow2 ? sh * w : sh / (float)i);
     }
-    color = add(color, divs(mul(h.color, prevColor), (float)i));
+    // x / i as x * 2^-k for i = 1, 2, 4: the same correctly rounded value (rm_kernels.hip bounce)
+    const f3 tw = mul(h.color, prevColor);
+    if (pow2) color = add(color, muls(tw, w));
+    else color = add(color, divs(tw, (float)i));
     prevColor = h.color;
     prevMat = h.material;
   }
