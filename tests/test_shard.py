@@ -140,3 +140,88 @@ def test_bench_broadcasts_rccl_ids_over_gloo(rm):
     assert got[0] == got[1]
     assert len(got[0]) == 3 and len(set(got[0])) == 3
     assert all(len(i) == rm.COMM_ID_BYTES for i in got[0])
+
+
+class _FakeRenderer:
+    """Stands in for a communicator context on the CPU: what rm_comm_rccl_info and
+    rm_frame_phases would report for rank `rank` of `world` (the reporting logic of
+    bench.py's N > 1 line is host code; the librm calls behind it run in
+    tests/test_gpu_bench_dist.py)."""
+
+    def __init__(self, rank, world, count=None):
+        self.rank, self.world, self.count = rank, world, world if count is None else count
+        self.n = 0
+
+    def rccl_info(self):
+        return {"count": self.count, "user_rank": self.rank, "hip_device": self.rank, "version": 22707}
+
+    def enable_timing(self, on):
+        pass
+
+    def kernel_time_ms(self, reset=False):
+        return 0.0, 0
+
+    def dispatch(self, u):
+        self.n = 1
+
+    def dispatch_frames(self, us):
+        self.n = len(us)
+
+    def frame_phases(self):
+        # per-rank render times differ: rank 1 is the slow one
+        return {"render_ms": 0.1 * self.n * (1 + self.rank), "gather_ms": 0.02 * self.n,
+                "assemble_ms": 0.01 * self.n if self.rank == 0 else 0.0}
+
+
+def _report_worker(rank, world, port, q, bad_count):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "opengl-raymarching-in-compute-shader_amd"))
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rs = [_FakeRenderer(rank, world, count=1 if (bad_count and rank == 1) else None) for _ in range(3)]
+    frames = bench.bench_frames(8)
+    out = {"rccl": bench.rccl_report(rs, rank, world),
+           "ph1": bench.frame_phase_stats(rs[0], frames, lambda f: f, 1, rank, world),
+           "ph4": bench.frame_phase_stats(rs[0], frames, lambda f: f, 4, rank, world)}
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_count", [False, True])
+def test_bench_n_gt_1_report_over_gloo(bad_count):
+    """VERDICT r03 #1 (world size 2, gloo): the N > 1 line's `rccl` object gathers
+    every communicator of every rank and flags a communicator RCCL formed with the
+    wrong size (a rank that rendered alone), and `phases` gives per-rank mean and
+    max over every timed frame (per frame also when the frames go in batches)."""
+    import multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_report_worker, args=(r, world, port, q, bad_count)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rc = got[0]["rccl"]
+    assert rc == got[1]["rccl"] and rc["world_size"] == 2 and len(rc["per_rank"]) == 2
+    assert all(len(p["comms"]) == 3 for p in rc["per_rank"])
+    if bad_count:
+        assert rc["nranks_seen"] == [1, 2] and not rc["all_communicators_match"]
+    else:
+        assert rc["nranks_seen"] == [2] and rc["all_communicators_match"] and rc["version"] == 22707
+    for key, batch in (("ph1", 1), ("ph4", 4)):
+        ph = got[0][key]
+        assert ph["frames"] == 8 and ph["frames_per_sample"] == batch
+        assert [p["rank"] for p in ph["per_rank"]] == [0, 1]
+        # per frame: the fake reports n x per-frame values, divided back by the batch
+        assert abs(ph["max_render_mean_ms"] - 0.2) < 1e-9 and abs(ph["max_render_max_ms"] - 0.2) < 1e-9
+        assert abs(ph["per_rank"][0]["render_mean_ms"] - 0.1) < 1e-9
+        assert abs(ph["assemble_mean_ms"] - 0.01) < 1e-9 and abs(ph["max_gather_mean_ms"] - 0.02) < 1e-9
