@@ -183,7 +183,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     asm volatile("" : "+v"(t), "+v"(dl));  // re-form the test, not a lane mask kept per step
     if (dl < 0.000001f * t) {
       const f3 q = add(ro, muls(rd, t));
-      id = lazy_id(lc, t);
+      id = lazy_id(lc, t, dl, ro.y, rd.y);
       col = hit_color(id, q);
       dlast = dl;
       return t;
@@ -239,7 +239,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   if (hit) {
     // the opU id (and colour) of the hit: from the last step's sdf (same point)
     const f3 q = add(ro, muls(rd, t));
-    id = lazy_id(lc, t);
+    id = lazy_id(lc, t, dl, ro.y, rd.y);
     col = hit_color(id, q);
     if (COUNT && proven_miss) col = mk(__builtin_nanf(""), 0.0f, 0.0f);
     dlast = dl;

@@ -446,8 +446,7 @@ struct LazyCull {
   float s0, s1;  // slack(t) = s0 + s1 t >= 2^-14 (|ro|_1 + |rd| t + 64)  (rounded up)
   float inv2v;   // (1 - 2^-10) / (2 |rd|)  (rounded down)
   float invp;    // (1 - 2^-10) / (|rd| + rd.y)  (rounded down)
-  float tb;      // t of the last step that entered the re-test block
-  int idb;       // the opU id found there
+  int idb;       // the opU id among the primitives the last block evaluated (7: none taken)
 };
 
 // Step 0 of every primary ray is the same computation: castRay starts all of
@@ -493,7 +492,6 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
   c.s0 = s0;
   c.s1 = s1;
-  c.tb = -1.0f;
   c.idb = 7;
 }
 
@@ -505,8 +503,16 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
 // is lazy_id(): the primitives are taken in the reference's order with ties
 // going to the later one, the plane last; culled primitives are strictly above
 // the minimum and can neither win nor tie.  A step that skips the block has
-// only the plane left: id 7.  (The block records its id with the step's t; t
-// strictly increases along a march, so tb == t identifies the step.)
+// only the plane left: id 7.  The block records its primitives' winner (idb);
+// the plane, last in the chain, wins a tie with it.  So at the hit step, whose
+// distance d is not NaN (d < 1e-6 t), the id is 7 exactly when d equals the
+// step's plane value: a step that skipped the block returns the plane value
+// itself, and a step that entered it returns the plane value only when no
+// primitive is strictly below it.  Otherwise the block ran at this very step
+// and idb is its winner.  lazy_id re-forms the plane value with the same
+// operations once per hit, where the block used to record the step's t and
+// compare and select at every entry (round 4: ~2.5 issue slots per entry, 13
+// entries per wave).
 // The point is p = ro + rd t (the march's q); only p.y is needed outside the
 // re-test block, so p.x / p.z are formed inside it.
 __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc, float blend,
@@ -515,7 +521,6 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
   float m = py + 5.5f;  // plane, exact (glsl:85,121); running minimum
   RM_STAT(8);
   if (__any(t >= lc.temin)) {
-    const float plane = m;
     int idp = 7;
 
     RM_STAT(9);
@@ -598,12 +603,16 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     }
     lc.tegrp = vmin(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[4]);
     lc.temin = vmin(lc.tegrp, lc.te[3]);
-    lc.idb = (m == plane) ? 7 : idp;  // no primitive strictly below the plane
-    lc.tb = t;
+    lc.idb = idp;  // (the plane's tie rule and the step: lazy_id)
   }
   return m;
 }
-__device__ __forceinline__ int lazy_id(const LazyCull& lc, float t) { return lc.tb == t ? lc.idb : 7; }
+// The hit's id: the block's winner unless the hit step's distance d is its
+// plane value (ro.y + rd.y t) + 5.5, formed as scene_lazy forms it (above).
+__device__ __forceinline__ int lazy_id(const LazyCull& lc, float t, float d, float roy, float rdy) {
+  const float plane = (roy + rdy * t) + 5.5f;
+  return d != plane ? lc.idb : 7;
+}
 
 // ---- provable early exits (softshadow, misses) ---------------------------------------
 // With C, R_ALL a sphere enclosing all five bounded primitives and
