@@ -55,6 +55,7 @@ struct rm_ctx {
   unsigned long long* d_counters = nullptr;
   float* d_uv = nullptr;          // per-column / per-row uv table (Frame::uvx / uvy)
   bool uv_exact = false;          // lane_uv's arithmetic equals the table (uv_exact_check)
+  float uv_lo[2] = {0, 0}, uv_hi[2] = {0, 0};  // range of the table's column / row values
   uint32_t* d_scene = nullptr;    // runtime scene table (rm_set_scene), compiled words
   int nprims = 0;                 // 0: the built-in scene and its specialised kernel
   std::vector<rm_primitive> scene;     // the table as given (rm_get_scene)
@@ -448,6 +449,49 @@ void table_prep_host(const uint32_t* words, int32_t n, const float cam[3], float
   }
 }
 
+// Frame::unit_rd: every primary ray of the frame has |rd| within 2^-20 of 1.
+// castRay (glsl:68-74) normalises v = uvx X + uvy Y + RN(D persp) (vec4, then
+// .xyz): with the w components of X, Y, D zero, v.w = +-0 and, when |v|^2 stays
+// in the normal range, every operation of normalize() has relative error <= u =
+// 2^-24, so |rd| is within ~4.5u of 1.  The host bounds |v|^2 over the uv table's
+// range [uv_lo, uv_hi]^2 exactly (a quadratic in (uvx, uvy): corners, edges and
+// the interior critical point, in double), and requires min |v|^2 >= 2^-38 M^2
+// (the float error of v, <= 3 sqrt(3) u M with M >= |v| the triangle bound,
+// then moves |v| by < 16 %), min |v|^2 >= 2^-80 and M^2 <= 2^100.
+static bool unit_rd_check(const rm_ctx* c, const rm_uniforms& u, float persp) {
+  const rm_camera& k = u.camera;
+  if (k.xAxis[3] != 0.0f || k.yAxis[3] != 0.0f || k.dir[3] != 0.0f) return false;
+  double X[3], Y[3], C[3];
+  for (int i = 0; i < 3; ++i) {
+    X[i] = k.xAxis[i];
+    Y[i] = k.yAxis[i];
+    C[i] = (double)(k.dir[i] * persp);  // the kernel's float product
+    if (!std::isfinite(X[i]) || !std::isfinite(Y[i]) || !std::isfinite(C[i])) return false;
+  }
+  auto dotd = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  const double xx = dotd(X, X), yy = dotd(Y, Y), xy = dotd(X, Y), xc = dotd(X, C), yc = dotd(Y, C),
+               cc = dotd(C, C);
+  auto q = [&](double a, double b) { return a * a * xx + b * b * yy + 2 * a * b * xy + 2 * a * xc + 2 * b * yc + cc; };
+  const double a0 = c->uv_lo[0], a1 = c->uv_hi[0], b0 = c->uv_lo[1], b1 = c->uv_hi[1];
+  if (!(a0 <= a1) || !(b0 <= b1)) return false;
+  auto clampd = [](double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); };
+  double m = std::fmin(std::fmin(q(a0, b0), q(a0, b1)), std::fmin(q(a1, b0), q(a1, b1)));
+  for (double a : {a0, a1})
+    if (yy > 0) m = std::fmin(m, q(a, clampd(-(a * xy + yc) / yy, b0, b1)));
+  for (double b : {b0, b1})
+    if (xx > 0) m = std::fmin(m, q(clampd(-(b * xy + xc) / xx, a0, a1), b));
+  const double det = xx * yy - xy * xy;
+  if (det > 0) {
+    const double a = (-xc * yy + yc * xy) / det, b = (-yc * xx + xc * xy) / det;
+    if (a >= a0 && a <= a1 && b >= b0 && b <= b1) m = std::fmin(m, q(a, b));
+  }
+  const double M = std::fmax(std::fabs(a0), std::fabs(a1)) * std::sqrt(xx) +
+                   std::fmax(std::fabs(b0), std::fabs(b1)) * std::sqrt(yy) + std::sqrt(cc);
+  // (m carries the double rounding of the quadratic, relative ~1e-15 of M^2:
+  // the 2^-38 M^2 floor is far above it)
+  return m >= std::ldexp(M * M, -38) && m >= std::ldexp(1.0, -80) && M * M <= std::ldexp(1.0, 100);
+}
+
 rmd::Frame make_frame(const rm_ctx* c) {
   const rm_uniforms& u = c->u;
   rmd::Frame F;
@@ -475,6 +519,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.uvx = c->d_uv;
   F.uvy = c->d_uv + (size_t)5 * c->cfg.width;
   F.uv_exact = c->uv_exact ? 1 : 0;
+  F.unit_rd = unit_rd_check(c, u, F.persp) ? 1 : 0;
   const float uv_ox[4] = {0.25f, 0.75f, 0.25f, 0.75f}, uv_oy[4] = {0.25f, 0.25f, 0.75f, 0.75f};
   for (int a = 0; a < 2; ++a) {
     const float n = (float)(a ? c->cfg.height : c->cfg.width);
@@ -914,6 +959,16 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     // lane_uv (rm_scene.hpp) may form the same values arithmetically when, for every
     // column and row, RN(1/n)-times-a plus one fma remainder correction equals the
     // IEEE (2p - n) / n; the offsets' adds are the table's own operations
+    for (int a = 0; a < 2; ++a) {
+      c->uv_lo[a] = INFINITY;
+      c->uv_hi[a] = -INFINITY;
+    }
+    for (int p = 0; p < W + H; ++p)
+      for (int k = 0; k < 5; ++k) {
+        const int a = p < W ? 0 : 1;
+        c->uv_lo[a] = std::fmin(c->uv_lo[a], uv[(size_t)p * 5 + k]);
+        c->uv_hi[a] = std::fmax(c->uv_hi[a], uv[(size_t)p * 5 + k]);
+      }
     c->uv_exact = true;
     for (int p = 0; p < W + H && c->uv_exact; ++p) {
       const bool col = p < W;

@@ -44,7 +44,12 @@ __device__ __forceinline__ float opaque(float x) {
 __device__ __forceinline__ f3 opaque(f3 v) { return mk(opaque(v.x), opaque(v.y), opaque(v.z)); }
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161.  Returns t or -1.
-template <bool COUNT>
+// UNIT: a primary ray of a frame whose rays all have |rd| within 2^-20 of 1
+// (Frame::unit_rd, checked on the host): |rd| = 1 serves every bound that
+// needs |rd| from below or above, with the bounds' own 2^-12 / 2^-16 margins
+// (it stood for a v_sqrt within 1.5 ulp), so |rd|, its reciprocal and the
+// slack slope become constants and the miss exit's object bound is uniform.
+template <bool COUNT, bool UNIT = false>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
                        float& dlast) {
   float t = 0.0f, dl = 0.0f;
@@ -54,14 +59,15 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
   // per-ray constants; the ro-dependent ones of primary rays come from the host
   // (rm_api.hip prep_host: every primary ray starts at the camera)
   const bool prep = !reflected && F.prepv[PREP_VALID] != 0.0f;
-  const float rdl = ray_rdl(rd), s1 = ray_s1(rdl);
+  const float rdl = UNIT ? 1.0f : ray_rdl(rd), s1 = ray_s1(rdl);
   const float s0 = prep ? F.prepv[PREP_SLACK] : ray_s0(ro);
   // ro in VGPRs: a primary ray's ro is the camera, uniform, and an SGPR operand
   // keeps an f32 add / mul from dual issue (4 instead of 2 cycles per wave64
   // instruction on gfx950, tools/valu_peak.hip), once per march step here.
   ro = opaque(ro);
   LazyCull lc;
-  lazy_init(lc, rd, rdl, s0, s1);
+  if (UNIT) lazy_init_unit(lc, rd, s0, s1);
+  else lazy_init(lc, rd, rdl, s0, s1);
   // the provable-miss threshold mx (rm_scene.hpp "early exits"), formed where it
   // is used: its ro-dependent terms b1, b2 with it (a downward ray has mx = +inf,
   // so waves of downward rays never form either)
@@ -81,7 +87,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     float b1c, b2c;
     if (prep) b1c = F.prepv[PREP_B1];
     else lin_exit_b(o, lc.s0, 0.0f, b1c, b2c);
-    return lin_exit_T1(MISS_C, ray_rdl(r), lc.s1, b1c);
+    return lin_exit_T1(MISS_C, UNIT ? 1.0f : ray_rdl(r), lc.s1, b1c);
   };
   // provable miss: production stops there; the counting build runs on to the
   // reference's step count and poisons the colour with NaN should the ray hit
@@ -362,7 +368,9 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   int id;
   f3 hcol;
   float dl;
-  float th = march<COUNT>(F, ro, rd, false, id, hcol, c, dl);
+  // (F.unit_rd is uniform: one march or the other for the whole wave)
+  float th = F.unit_rd ? march<COUNT, true>(F, ro, rd, false, id, hcol, c, dl)
+                       : march<COUNT, false>(F, ro, rd, false, id, hcol, c, dl);
 #ifdef RM_DBL_MARCH
   if (!COUNT) {
     int id2; f3 hc2; float dl2;

@@ -87,6 +87,7 @@ struct Frame {
   float uv_dims[2];      // W, H as floats
   float uv_off[2][4];    // RN(ox_k / W), RN(oy_k / H)
   int32_t uv_exact;
+  int32_t unit_rd; // every primary rd of this frame has |rd| within 2^-20 of 1 (host check, march)
   int32_t bounces; // bounceVar, 0..5
   int32_t aa;      // AA
   int32_t width, height;
@@ -490,6 +491,23 @@ __device__ __forceinline__ void lazy_init(LazyCull& c, f3 rd, float rdl, float s
   // rdlen over-estimates |rd| by >= 2^-17 |rd|, so the rounded sum is above
   // the true |rd| + rd.y even under cancellation; its reciprocal may be large.
   c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(rdlen + rd.y) * (1.0f - 0x1p-16f);
+  c.s0 = s0;
+  c.s1 = s1;
+  c.idb = 7;
+}
+
+// lazy_init for |rd| within 2^-20 of 1 (Frame::unit_rd): rdlen = 1 + 2^-16 >= |rd|
+// (over by >= 2^-17 |rd|), so inv2v is the constant (1/2)(1 - 2^-10)/(1 + 2^-16)
+// rounded down (the rcp form's (1 - 2^-16) factor covered its 1 ulp).
+__device__ __forceinline__ void lazy_init_unit(LazyCull& c, f3 rd, float s0, float s1) {
+  const float NEG = -__builtin_huge_valf();
+#pragma unroll
+  for (int k = 0; k < 5; ++k) c.te[k] = NEG;
+  c.temin = NEG;
+  c.tegrp = NEG;
+  constexpr float RDLEN = 1.0f + 0x1p-16f;
+  c.inv2v = 0x1.ff7ep-2f;  // 0.5 (1 - 2^-10) / (1 + 2^-16) = 0.499504097 rounded down
+  c.invp = (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(RDLEN + rd.y) * (1.0f - 0x1p-16f);
   c.s0 = s0;
   c.s1 = s1;
   c.idb = 7;
