@@ -276,20 +276,21 @@ __device__ f3 get_normal(const Frame& F, f3 pos, Cnt& c, float c0 = 0.0f) {
 
 // softshadow glsl:201-216
 template <bool COUNT>
-__device__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c);
+__device__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, float rdl, Cnt& c);
+// rdl: |rd| (the light term's exact distance, shadow_exit_init)
 template <bool COUNT>
-__device__ __forceinline__ float softshadow(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+__device__ __forceinline__ float softshadow(const Frame& F, f3 ro, f3 rd, float rdl, Cnt& c) {
 #ifdef RM_DBL_SHADOW
-  if (!COUNT) return vmin(softshadow_impl<COUNT>(F, ro, rd, c), softshadow_impl<COUNT>(F, opaque(ro), rd, c));
+  if (!COUNT) return vmin(softshadow_impl<COUNT>(F, ro, rd, rdl, c), softshadow_impl<COUNT>(F, opaque(ro), rd, rdl, c));
 #endif
-  return softshadow_impl<COUNT>(F, ro, rd, c);
+  return softshadow_impl<COUNT>(F, ro, rd, rdl, c);
 }
 template <bool COUNT>
-__device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, Cnt& c) {
+__device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, float rdl, Cnt& c) {
   float res = 1.0f, t = 0.0f;
   int dummy;
   RM_STAT(29);
-  const float ex = shadow_exit_init(F.shc, ro, rd);
+  const float ex = shadow_exit_init(F.shc, ro, rd, rdl);
   for (int i = 0; i < 16; ++i) {
     if (lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;
@@ -321,6 +322,7 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     int id;
     f3 tcol;
     float dl;
+    float ldist;  // set with the light term; read only after a hit on the floor (id 7)
     float th = march<COUNT>(F, add(pos, muls(normal, 0.001f)), rayDir, true, id, tcol, c, dl);
 #ifdef RM_DBL_BMARCH
     if (!COUNT) {
@@ -337,7 +339,7 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
       tcol = subs(mk(0.36f, 0.36f, 0.60f), rayDir.y * 0.2f);
     } else {
       if (COUNT) c.lights++;
-      tcol = point_light(F, tcol, normal, pos);
+      tcol = point_light(F, tcol, normal, pos, &ldist);
     }
     // The weights x / i (glsl:186-187).  For i = 1, 2, 4 the quotient is the
     // real number x * 2^-k, exactly representable unless it underflows, and
@@ -349,7 +351,7 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
     const bool pow2 = (i & (i - 1)) == 0;
     const float w = i == 1 ? 1.0f : (i == 2 ? 0.5f : 0.25f);
     if (id == 7 && !prevMatte && i < 3) {
-      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), ldist, c);
       color = muls(color, pow2 ? sh * w : div_small(sh, i));
     }
     const f3 tw = mul(tcol, prevColor);
@@ -384,7 +386,8 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
     f3 pos = add(ro, muls(rd, th));
     f3 normal = get_normal<COUNT, true>(F, pos, c, dl);
     if (COUNT) c.lights++;
-    color = point_light(F, hcol, normal, pos);
+    float ldist;
+    color = point_light(F, hcol, normal, pos, &ldist);
 #ifdef RM_DBL_LIGHT
     if (!COUNT) {
       const f3 c2 = point_light(F, hcol, normal, opaque(pos));
@@ -393,7 +396,7 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 #endif
     if (id == 7) {
       f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
-      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
+      float sh = softshadow<COUNT>(F, add(pos, muls(normal, 0.02f)), sub(lpos, pos), ldist, c);
       color = muls(color, sh);
       return gamma(color);
     }

@@ -680,8 +680,8 @@ __device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float
   return (a1 > 0.0f && a2 > 0.0f) ? __builtin_fmaxf(T1, T2) : INF;
 }
 constexpr float MISS_C = 0.000001f * (1.0f + 0x1p-9f);
-__device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd) {
-  const float rdl = ray_rdl(rd), s0 = ray_s0(ro);
+__device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd, float rdl) {
+  const float s0 = ray_s0(ro);
   float b1, b2;
   lin_exit_b(ro, s0, hmin, b1, b2);
   return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2);
@@ -690,10 +690,14 @@ __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd
 // with the same float operations once per frame (rm_api.hip make_frame), where
 // the device would have spent a full IEEE division (~14 VALU) per shadow call
 // site and wave on a uniform value.
-__device__ __forceinline__ float shadow_exit_init(float c, f3 ro, f3 rd) {
-  return lin_exit_init(c, 0.001f, ro, rd);
+// rdl: |rd| within 1.5 ulp.  A shadow ray's rd is light - pos, whose exact
+// length the light term at the same pos has already formed (point_light's
+// `distance`, correctly rounded): the caller passes it instead of a v_sqrt
+// (round 4).
+__device__ __forceinline__ float shadow_exit_init(float c, f3 ro, f3 rd, float rdl) {
+  return lin_exit_init(c, 0.001f, ro, rd, rdl);
 }
-__device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd); }
+__device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd, ray_rdl(rd)); }
 __device__ __forceinline__ bool lin_exit(float T, float t) { return t > T; }
 
 // ---- step-cap miss exit (RayMarch / reflectedRay, glsl:125-161) ---------------
@@ -786,7 +790,8 @@ __device__ __forceinline__ float gpow(float x, float y) {
 }
 
 // getPointLight glsl:253-276
-__device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f3 pos) {
+// dist_out: length(light - pos), the shadow ray's |rd| (shadow_exit_init).
+__device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f3 pos, float* dist_out = nullptr) {
   f3 lpos = mk(F.lpos[0], F.lpos[1], F.lpos[2]);
   f3 ambient = mk(F.lamb[0], F.lamb[1], F.lamb[2]);
   f3 viewDir = normalize(sub(pos, mk(F.cam_pos[0], F.cam_pos[1], F.cam_pos[2])));
@@ -797,6 +802,7 @@ __device__ __forceinline__ f3 point_light(const Frame& F, f3 color, f3 normal, f
   float spec = gpow(gmax(dot(viewDir, reflectDir), 0.0f), 32.0f);
   f3 specular = muls(mk(F.lspec[0], F.lspec[1], F.lspec[2]), spec);
   float distance = len(sub(lpos, pos));
+  if (dist_out) *dist_out = distance;
   float attenuation = rcp_exact((F.lconst + F.llin * distance) + F.lquad * (distance * distance));
   diffuse = muls(diffuse, attenuation);
   ambient = muls(ambient, attenuation);

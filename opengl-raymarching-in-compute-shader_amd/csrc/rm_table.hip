@@ -571,6 +571,11 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
       };
 #ifdef RM_TABLE_STATIC
       do {
+        // Every lane still marching has taken the same steps, so the step count
+        // is one scalar: re-read from the first active lane, since the compiler
+        // keeps a value leaving a loop with per-lane exits in a VGPR (a vector
+        // add and compare per step otherwise, round 4).
+        i = __builtin_amdgcn_readfirstlane(i);
         d = lz.dist(S, add(ro, muls(rd, t)), t, k);
         latch();
         while (!ex && !lz.due(t)) {
