@@ -571,11 +571,6 @@ __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected
       };
 #ifdef RM_TABLE_STATIC
       do {
-        // Every lane still marching has taken the same steps, so the step count
-        // is one scalar: re-read from the first active lane, since the compiler
-        // keeps a value leaving a loop with per-lane exits in a VGPR (a vector
-        // add and compare per step otherwise, round 4).
-        i = __builtin_amdgcn_readfirstlane(i);
         d = lz.dist(S, add(ro, muls(rd, t)), t, k);
         latch();
         while (!ex && !lz.due(t)) {
@@ -693,19 +688,17 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
       if (COUNT) c.lights++;
       h.color = point_light(F, h.color, normal, pos);
     }
-    const bool pow2 = (i & (i - 1)) == 0;  // wave-uniform: a scalar branch
-    const float w = i == 1 ? 1.0f : (i == 2 ? 0.5f : 0.25f);
+    // (x / i stays a division here: the built-in kernel's power-of-two products,
+    // rm_kernels.hip bounce, make the generic kernel spill 45 VGPRs -- 588 B of
+    // scratch per lane instead of 28, round 4)
     if (h.id == 7 && i < 3) {  // prevObject.material != MATTE here
       float sh = tshadow<COUNT, KL>(F, S, add(pos, muls(normal, 0.02f)), sub(lpos, pos), c);
 #ifdef RM_TDBL_SHADOW
       if (!COUNT) sh = fminf(sh, tshadow<COUNT, KL>(F, S, topaque(add(pos, muls(normal, 0.02f))), sub(lpos, pos), c));
 #endif
-      color = muls(color, pow2 ? sh * w : sh / (float)i);
+      color = muls(color, sh / (float)i);
     }
-    // x / i as x * 2^-k for i = 1, 2, 4: the same correctly rounded value (rm_kernels.hip bounce)
-    const f3 tw = mul(h.color, prevColor);
-    if (pow2) color = add(color, muls(tw, w));
-    else color = add(color, divs(tw, (float)i));
+    color = add(color, divs(mul(h.color, prevColor), (float)i));
     prevColor = h.color;
     prevMat = h.material;
   }
