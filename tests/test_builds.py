@@ -33,3 +33,39 @@ def test_diagnostic_build_compiles(name, tmp_path):
            "-o", str(tmp_path / "k.o")] + DIAG[name]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+BUILD = os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd", "build")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+# Scratch bytes per lane each production kernel may use: none for the built-in
+# kernels; the generic table kernel spills a few VGPRs (28 B at 8 slots since
+# round 3).  Round 4 found it at 588 B after a change to its bounce loop.
+# (keys: substrings of the mangled names -- k_pixel<false>, k_sample<false>, the
+# batched k_*_frames, k_table_*<false, KL>)
+SCRATCH_MAX = {"7k_pixelILb0E": 0, "8k_sampleILb0E": 0, "14k_pixel_frames": 0,
+               "15k_sample_frames": 0, "13k_table_pixelILb0E": 32, "14k_table_sampleILb0E": 32}
+
+
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not installed")
+@pytest.mark.parametrize("obj", ["rm_kernels.o", "rm_kernels_aa.o", "rm_table.o"])
+def test_production_kernels_scratch(obj, tmp_path):
+    """The in-tree build's gfx950 code objects (make librm, __graft_entry__.build):
+    the private segment of every production kernel, from its kernel descriptor."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_scene_table import _kernel_private_sizes
+    src = os.path.join(BUILD, obj)
+    if not os.path.exists(src):
+        pytest.skip("librm not built")
+    shutil.copy(src, tmp_path / "x.o")
+    subprocess.run([OBJDUMP, "--offloading", "x.o"], cwd=tmp_path, capture_output=True, check=True)
+    cos = [p for p in os.listdir(tmp_path) if "gfx950" in p]
+    assert len(cos) == 1, os.listdir(tmp_path)
+    priv = _kernel_private_sizes(open(tmp_path / cos[0], "rb").read())
+    seen = 0
+    for sym, size in priv.items():
+        for key, cap in SCRATCH_MAX.items():
+            if key in sym:
+                seen += 1
+                assert size <= cap, (sym, size, cap)
+    assert seen > 0, priv
