@@ -202,19 +202,21 @@ def comm_ids(n: int, rank: int) -> list:
     return ids
 
 
-def default_batch(config: int, dist_on: bool, one_comm: bool) -> int:
+def default_batch(config: int, dist_on: bool, one_comm: bool, steps: int) -> int:
     """Frames per launch when --batch is not given (measured).
 
     One GPU: cfg1 / cfg2 frames (4K / 32K one-wave workgroups) are shorter than their
-    longest waves and cannot fill 256 CUs alone; 10 frames per launch on 2 contexts
-    render at 0.0146 / 0.0653 ms per frame against 0.0593 / 0.0906 with 3 frames in
-    flight (round 4, tools/probe_batch.py).  The 4K / 8K supersampled frames fill the
-    chip by themselves; 3 frames in flight and batches measure the same there."""
+    longest waves and cannot fill 256 CUs alone.  Over the whole 120-frame sweep, 20
+    frames per launch on 3 contexts render at 0.0090 / 0.0575 ms per frame against
+    0.0124 / 0.0594 for 10 on 2 (round 4, tools/probe_batch.py --steps 120,
+    profiles/r04_probe_batch120.txt); fewer steps cap the batch so that the launches
+    still spread over the 3 contexts.  The 4K / 8K supersampled frames fill the chip
+    by themselves; 3 frames in flight and batches measure the same there."""
     if one_comm:
         return 4  # N > 1, one communicator: gather batch j while batch j + 1 renders
     if dist_on:
         return 1
-    return 10 if config in (1, 2) else 1
+    return max(1, min(20, -(-steps // 3))) if config in (1, 2) else 1
 
 
 def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
@@ -358,10 +360,10 @@ def main() -> int:
     # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
     # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
     one_comm = dist_on and args.comms == 1
-    batch = args.batch if args.batch > 0 else default_batch(args.config, dist_on, one_comm)
+    batch = args.batch if args.batch > 0 else default_batch(args.config, dist_on, one_comm, args.steps)
     batch = max(1, min(batch, rm.RM_MAX_BATCH, args.steps))
-    # contexts in flight: 3 frames on one GPU, 2 batches, 4 frames of a sharded step
-    nfl = args.inflight if args.inflight > 0 else ((2 if batch > 1 else 3) if not dist_on else 4)
+    # contexts in flight: 3 frames or batches on one GPU, 4 frames of a sharded step
+    nfl = args.inflight if args.inflight > 0 else (3 if not dist_on else 4)
     nfl = nfl if (not dist_on or args.pipeline) else 1
     if one_comm:
         nfl = 1  # one context, one communicator; batches overlap through its gather stream
