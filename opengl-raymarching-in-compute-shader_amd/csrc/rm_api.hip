@@ -547,6 +547,20 @@ rmd::Frame make_frame(const rm_ctx* c) {
   return F;
 }
 
+// The specialised table kernels for frame F, or null: they take sqrt(x) - R in
+// the fast exact form for march and normal points (rm_table.hip sqrt_sub), which
+// needs every such point within 2^53 of every entry.  Entries lie within 10^15
+// of the origin (rm::exit_bounds), a march moves at most nmax tmax = 2.05e5
+// along a unit ray and five bounces add 1.3e5 more, so a camera within 10^15
+// of the origin keeps them there; a frame whose camera is farther out (or not
+// finite) renders with the generic kernel.
+const rm::JitTable* frame_jit(const rm_ctx* c, const rmd::Frame& F) {
+  if (!c->jit) return nullptr;
+  for (int i = 0; i < 3; ++i)
+    if (!(std::fabs(F.cam_pos[i]) <= 1e15f)) return nullptr;
+  return c->jit;
+}
+
 void graph_release(rm_ctx* c) {
   rm_graph_slot& g = c->gs;
   if (g.exec || g.graph) (void)hipStreamSynchronize(c->stream);
@@ -1112,8 +1126,9 @@ int render_launch(rm_ctx* c) {
   if ((rc = timing_events(c, &e0, &e1)) != RM_OK) return rc;
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   // a runtime scene table renders with the table kernel
-  hipError_t e = c->nprims ? (c->jit ? rm::launch_table_jit(c->jit, F, c->cfg.counters != 0, c->stream)
-                                      : rm::launch_table(F, c->cfg.counters != 0, c->stream, table_slots(c)))
+  const rm::JitTable* jit = frame_jit(c, F);
+  hipError_t e = c->nprims ? (jit ? rm::launch_table_jit(jit, F, c->cfg.counters != 0, c->stream)
+                                  : rm::launch_table(F, c->cfg.counters != 0, c->stream, table_slots(c)))
                            : rm::launch_pixel(F, c->cfg.counters != 0, c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
@@ -1226,8 +1241,9 @@ int launch_batch(rm_ctx* c, const rm_uniforms* u, int n, O8 out8, O32 out32) {
     F.sdf_counts = nullptr;
     F.counters = nullptr;
     if (c->nprims) {
-      const hipError_t e = c->jit ? rm::launch_table_jit(c->jit, F, false, c->stream)
-                                  : rm::launch_table(F, false, c->stream, table_slots(c));
+      const rm::JitTable* jit = frame_jit(c, F);
+      const hipError_t e = jit ? rm::launch_table_jit(jit, F, false, c->stream)
+                               : rm::launch_table(F, false, c->stream, table_slots(c));
       if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
       continue;
     }
@@ -1589,7 +1605,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess) {
     e = !F.nprims ? rm::launch_pixel(F, false, cs)
-        : c->jit  ? rm::launch_table_jit(c->jit, F, false, cs)
+        : frame_jit(c, F) ? rm::launch_table_jit(frame_jit(c, F), F, false, cs)
                   : rm::launch_table(F, false, cs, table_slots(c));
     // the render node: the one node the next captured operation would depend on
     hipStreamCaptureStatus st;
@@ -1620,7 +1636,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   g.frame = image_rgba8(c);
   c->graph_aa = F.aa;
   c->graph_table = table_key(c);
-  c->graph_jit = F.nprims ? c->jit : nullptr;
+  c->graph_jit = F.nprims ? frame_jit(c, F) : nullptr;
   return RM_OK;
 }
 
@@ -1661,7 +1677,7 @@ int graph_frame(rm_ctx* c) {
     return rm_dispatch(c);
   }
   if ((F.aa != c->graph_aa || table_key(c) != c->graph_table ||
-       (F.nprims ? c->jit : nullptr) != c->graph_jit || c->gs.send != render_dst(c) ||
+       (F.nprims ? frame_jit(c, F) : nullptr) != c->graph_jit || c->gs.send != render_dst(c) ||
        c->gs.frame != image_rgba8(c)) &&
       (rc = graph_capture(c, F)) != RM_OK)
     return rc;

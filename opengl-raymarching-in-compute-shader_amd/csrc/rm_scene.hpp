@@ -53,6 +53,11 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) {
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -438,8 +443,14 @@ __device__ __forceinline__ void normal_samples(f3 pos, float blend, float omblen
 // plane(p_j) = plane(p_i) + rd.y (t_j - t_i), and min(p_j) <= plane(p_j), so k
 // also stays above the minimum while
 //   t_j < t_i + (LB_k - plane(p_i) - slack) / (|rd| + rd.y) * (1 - 2^-10)
-// (|rd| + rd.y >= 0; level and downward rays get 2x and more).  te_k is the
-// later of the two expiries; both are valid, so their max is.
+// (|rd| + rd.y >= 0; level and downward rays get 2x and more).  Any valid
+// expiry will do, and the later of several is valid too.  Step 0 of a primary
+// ray (host gaps, PREP_G / PREP_H) takes the later of both; the block's
+// re-tests take the plane budget alone (round 4): where U_i is the plane, the
+// plane budget is the longer one (1 / (|rd| + rd.y) >= 1 / (2 |rd|)), and
+// forming the first costs two subtractions and an fma per re-test, more than
+// the re-tests it saves where a primitive is nearer than the plane (cfg3
+// -1.1 %, cfg2 -2.8 % per frame, tools/patches/plane_budget_only.diff A/B).
 struct LazyCull {
   float te[5];   // expiry t of spheres 0/1, blend, torus, capsule
   float temin;   // min over te[]
@@ -543,7 +554,7 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
 
     RM_STAT(9);
     const float slack = __builtin_fmaf(lc.s1, t, lc.s0);
-    const float inv2v = lc.inv2v, invp = lc.invp;
+    const float invp = lc.invp;
     const float pl = m + slack;  // plane(p_i) + slack
     // The opU id among the evaluated primitives, later wins ties, compared with
     // the running minimum m (plane included) rather than a separate minimum over
@@ -560,20 +571,19 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       RM_STAT(1);
       RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
-      const float g = lb - m - slack;
-      // The new expiry is the latest of the old one and the two budgets' ends;
-      // both budgets and the old expiry are valid, so their max is.  g <= 0 makes
-      // both budgets end at or before t (plane >= m), leaving an expired lane
-      // with te <= t: evaluated now and re-tested at its next step, whatever the
-      // exact value below t.  An idle lane keeps its te > t.  The fmas round once
-      // instead of twice (t + g b rather than t + RN(g b)), inside the budgets'
-      // 2^-10 margin.  One v_max3 (the float max: a te below t may be negative)
-      // replaces max3(b1, b2, t) followed by max(te, .) (round 3: one issue slot).
-      te = vmax3(__builtin_fmaf(g, inv2v, t), __builtin_fmaf(lb - pl, invp, t), te);
+      // The new expiry is the later of the old one and the plane budget's end;
+      // both are valid, so their max is.  A gap lb - pl <= 0 ends the budget at
+      // or before t, leaving an expired lane with te <= t: evaluated now and
+      // re-tested at its next step, whatever the exact value below t.  An idle
+      // lane keeps its te > t.  The fma rounds once instead of twice (t + g b
+      // rather than t + RN(g b)), inside the budget's 2^-10 margin.  The float
+      // max (a te below t may be negative) without t among its operands: a te
+      // below t is as expired as te = t (round 3).
+      te = vmax(__builtin_fmaf(lb - pl, invp, t), te);
       // Evaluate exactly when the new expiry does not pass t: an expired lane
-      // whose budgets are <= 0, and also one whose tiny g > 0 cannot move t --
-      // an extra exact evaluation, never a wrong skip.  One compare instead of
-      // two (`expired & !(g > 0)`, round 3).
+      // whose gap is <= 0, and also one whose tiny gap > 0 cannot move t -- an
+      // extra exact evaluation, never a wrong skip.  One compare instead of two
+      // (`expired & !(g > 0)`, round 3).
       return te <= t;
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);

@@ -61,6 +61,14 @@ struct No { static constexpr bool value = false; };
 
 using rm::TABLE_WORDS;
 
+// The specialised kernels only render frames whose march and normal points are
+// bounded (prim_dist's BOUNDED form; rm_api.hip frame_jit).
+#ifdef RM_TABLE_STATIC
+constexpr bool kBoundedPoints = true;
+#else
+constexpr bool kBoundedPoints = false;
+#endif
+
 // Wave vote on the ballot builtin itself (hiprtc's __any widens the predicate
 // to an int and compares it again: two extra VALU per vote).
 __device__ __forceinline__ bool wany(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
@@ -80,7 +88,23 @@ __device__ __forceinline__ float tlen(f3 a) { return isqrt_ieee(dot(a, a)); }
 // GLSL normalize over the full float range (v * (1 / sqrt(dot)))
 __device__ __forceinline__ f3 tnormalize(f3 a) { return muls(a, 1.0f / isqrt_ieee(dot(a, a))); }
 
+// sqrt(x) - R as the IEEE operations give it.  BOUNDED: a specialised table's
+// march and normal points, within 2^53 of every entry's centre (the host renders
+// a frame whose camera is farther than 10^15 from the origin with the generic
+// kernel, rm_api.hip frame_jit; entries lie within 10^15, rm::exit_bounds; a
+// march moves at most nmax tmax along a unit ray, 5 bounces add 5 x 256 x 200),
+// so x is a finite sum of squares, and for a compile-time R >= 2^-20 sqrt_core
+// alone is exact: on [2^-96, FLT_MAX] it is the correctly rounded sqrt
+// (rm_fastmath.hpp); below, both roots are under 2^-47, inside half an ulp of R,
+// and both differences round to -R.  Otherwise the full-range form.
+template <bool BOUNDED>
+__device__ __forceinline__ float sqrt_sub(float x, float R) {
+  if (BOUNDED && R >= 0x1p-20f) return sqrt_core(x) - R;
+  return isqrt_ieee(x) - R;
+}
+
 // One table entry's distance at p (glsl:83-103, 115-121).
+template <bool BOUNDED = false>
 __device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float blend,
                                            float omblend) {
   f3 q = sub(p, mk(P[rm::TW_CENTER], P[rm::TW_CENTER + 1], P[rm::TW_CENTER + 2]));
@@ -88,24 +112,25 @@ __device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float
   const float* a = P + rm::TW_P;
   switch (type) {
     case RM_PRIM_SPHERE:
-      return tlen(q) - a[0];
+      return sqrt_sub<BOUNDED>(dot(q, q), a[0]);
     case RM_PRIM_BOX:
     case RM_PRIM_BLEND: {
       const f3 d = mk(fabsf(q.x) - a[0], fabsf(q.y) - a[1], fabsf(q.z) - a[2]);
       const f3 m = mk(gmax(d.x, 0.0f), gmax(d.y, 0.0f), gmax(d.z, 0.0f));
       const float box = gmin(gmax(d.x, gmax(d.y, d.z)), 0.0f) + tlen(m);
       if (type == RM_PRIM_BOX) return box;
-      const float sph = tlen(q) - a[3];
+      const float sph = sqrt_sub<BOUNDED>(dot(q, q), a[3]);
       return box * omblend + sph * blend;  // mix(box, sphere, blend)
     }
     case RM_PRIM_TORUS: {
-      const float l = isqrt_ieee(q.x * q.x + q.z * q.z) - a[0];
-      return isqrt_ieee(l * l + q.y * q.y) - a[1];
+      const float l = sqrt_sub<BOUNDED>(q.x * q.x + q.z * q.z, a[0]);
+      return sqrt_sub<BOUNDED>(l * l + q.y * q.y, a[1]);
     }
     case RM_PRIM_CAPSULE: {
       const f3 pa = sub(q, mk(a[0], a[1], a[2])), ba = mk(a[3], a[4], a[5]);
       const float h = gmin(gmax(dot(pa, ba) / a[6], 0.0f), 1.0f);
-      return tlen(sub(pa, muls(ba, h))) - a[7];
+      const f3 r = sub(pa, muls(ba, h));
+      return sqrt_sub<BOUNDED>(dot(r, r), a[7]);
     }
     default:  // RM_PRIM_PLANE
 #ifdef RM_TABLE_STATIC
@@ -246,7 +271,7 @@ struct Table {
       RM_TS_UNROLL
       for (int k = 0; k < n; ++k) {
         if (!((keep >> k) & 1u)) continue;
-        const float v = prim_dist(entry(k), type(k), q, blend, omblend);
+        const float v = prim_dist<kBoundedPoints>(entry(k), type(k), q, blend, omblend);
         d = d < v ? d : v;
       }
       return d;
@@ -505,10 +530,179 @@ struct THit {
   float d;  // a hit's last distance: sdf at the hit point itself (GetNormal's centre sample)
 };
 
+#ifdef RM_TABLE_STATIC
+// ---- the built-in kernel's march shape for reference-shaped tables -------------
+// A specialised table whose bounded entries all sit in lazy slots and whose one
+// plane is its last entry, axis-aligned (q.y n_y + w, as the reference's floor):
+// the production march then runs scene_lazy's block (rm_scene.hpp) over the
+// table instead of TLazy.  Per step only p.y and the plane value; the block is
+// entered when some lane's expiry passes t, forms p.x / p.z, the slack from a
+// line in t and re-tests the due slots in table order, evaluating an entry
+// exactly where its new expiry does not pass t.  Same values, fewer
+// instructions: the culling only skips entries proven strictly above the
+// minimum, as TLazy's.
+__device__ __forceinline__ bool slazy_table(const Table& S) {
+  const float* ex = S.exits();
+  const int kp = S.n - 1;
+  if (ex[rm::EX_VALID] == 0.0f || ex[rm::EX_NPLANES] != 1.0f || S.type(kp) != RM_PRIM_PLANE) return false;
+  const float* P = S.entry(kp);
+  if (__float_as_int(P[rm::TW_SWIZZLE]) != RM_SWIZZLE_XYZ) return false;
+  if (!(P[rm::TW_P] == 0.0f && P[rm::TW_P + 2] == 0.0f)) return false;
+  if ((int)ex[rm::EX_NSLOTS] != S.n - 1) return false;  // every other entry tracked ...
+  RM_TS_UNROLL
+  for (int j = 0; j < S.n - 1; ++j)
+    if ((int)ex[rm::EX_SLOTS + j] != j) return false;  // ... slot j holding entry j
+  return true;
+}
+
+// Expiries by TLazy's argument (above), in scene_lazy's form:
+//   * the slack is the line s0 + s1 t >= TLazy's sl(p(t)): |p|_1 <= (|ro|_1 +
+//     |rd|_1 t)(1 + 2^-22) for the float p, so sig2 (|p|_1 + |ro|_1 + S)(1 + 2^-10)
+//     <= sig2 (2 |ro|_1 + S)(1 + 2^-9) + sig2 |rd|_1 (1 + 2^-9) t; s0, s1 carry
+//     (1 + 2^-8) for their own roundings.  A larger slack gives a smaller gap.
+//   * the budget is the plane's: its value P is linear along the ray with slope
+//     n_y rd.y exactly and bounds the minimum from above (TLazy's U may be any
+//     such bound), so an entry whose gap (lb - P) - sl is positive stays above
+//     the minimum while the gap, shrinking at most at |rd| + n_y rd.y + s1 per
+//     unit of t, lasts (invp = 0 when that rate is not positive: no budget).
+//     TLazy's own budget, at rate inv, serves the host's step-0 gaps.
+//   * the exact evaluations of a step run inline in table order against the
+//     running minimum m (the plane first: it is the last entry and wins ties).
+template <int KL>
+struct SLazy {
+  float te[KL];
+  float temin, s0, s1, inv, invp;
+  int idb;  // the entry the last block's values made the winner (the plane: n - 1)
+};
+
+// The minimum over the first ns expiries (ns a compile-time count), three at a
+// time (v_min3_f32).
+template <int KL>
+__device__ __forceinline__ float slot_min(const float (&te)[KL], int ns) {
+  float m = te[0];
+  int j = 1;
+  RM_TS_UNROLL
+  for (; j + 1 < KL && j + 1 < ns; j += 2) m = vmin3(m, te[j], te[j + 1]);
+  RM_TS_UNROLL
+  for (; j < KL && j < ns; ++j) m = vmin(m, te[j]);
+  return m;
+}
+
+template <int KL>
+__device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflected, const float* prep) {
+  ro = topaque(ro);
+  const float* ex = S.exits();
+  const int ns = S.n - 1, kp = S.n - 1;
+  const float tmax = reflected ? 200.0f : 400.0f;
+  const int nmax = reflected ? 256 : 512;
+  const float T = table_exit_T(ex, MISS_C, 0.0f, ro, rd);
+  const float* PL = S.entry(kp);
+  // the plane's value at height y, prim_dist's float operations (q.x, q.z unused)
+  auto plane = [&](float y) { return prim_dist(PL, RM_PRIM_PLANE, mk(0.0f, y, 0.0f), S.blend, S.omblend); };
+  SLazy<KL> lz;
+  {
+    const float sig2 = 2.0f * ex[rm::EX_SIGMA];
+    const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+    const float rd1 = ((fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z)) * (1.0f + 0x1p-16f);
+    const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
+    lz.s0 = sig2 * (2.0f * ro1 + ex[rm::EX_S]) * ((1.0f + 0x1p-9f) * (1.0f + 0x1p-8f));
+    lz.s1 = sig2 * rd1 * ((1.0f + 0x1p-9f) * (1.0f + 0x1p-8f));
+    lz.inv = (1.0f - 0x1p-10f) *
+             __builtin_amdgcn_rcpf((1.0f + ex[rm::EX_LIP]) * rdl + sig2 * rd1) * (1.0f - 0x1p-16f);
+    // the plane's world normal is (0, n_y, 0): its slope along the ray is n_y rd.y
+    // (one rounding, far inside the 2^-8 added to s1)
+    const float ratep = (rdl + ex[rm::EX_PLANES + 1] * rd.y) + lz.s1 * (1.0f + 0x1p-8f);
+    lz.invp = ratep > 0.0f ? (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(ratep) * (1.0f - 0x1p-16f) : 0.0f;
+    lz.idb = kp;
+  }
+  float t = 0.0f, dl = 0.0f;
+  int i0 = 1;  // sdf evaluations the first loop step brings the count to
+  const float NEG = -__builtin_huge_valf();
+  if (prep && prep[rm::TP_VALID] != 0.0f) {
+    // step 0 at the camera, evaluated on the host (tmarch above); the gaps are
+    // TLazy's, their expiries at TLazy's rate
+    RM_TS_UNROLL
+    for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f) : __builtin_huge_valf();
+    dl = prep[rm::TP_D0];
+    t = dl;
+    i0 = 2;
+  } else {
+    RM_TS_UNROLL
+    for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? NEG : __builtin_huge_valf();
+  }
+  lz.temin = slot_min(lz.te, ns);
+  if (!(t <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
+
+  // sdf(ro + rd t): the plane, and the block when some lane's expiry has passed
+  auto step = [&](float tt) {
+    const float py = ro.y + rd.y * tt;
+    float m = plane(py);
+    if (wany(tt >= lz.temin)) {
+      const float sl = __builtin_fmaf(lz.s1, tt, lz.s0);
+      const float pl = m + sl;
+      const f3 p = mk(ro.x + rd.x * tt, py, ro.z + rd.z * tt);
+      int idp = kp;
+      RM_TS_UNROLL
+      for (int j = 0; j < KL; ++j) {
+        if (j >= ns || !wany(tt >= lz.te[j])) continue;
+        const float* B = S.entry(j) + rm::TW_BALL;
+        const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
+        const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
+                                        1.0f - 0x1p-12f, -B[3]);
+        // (the plane budget alone, as scene_lazy's re-test: rm_scene.hpp)
+        lz.te[j] = vmax(__builtin_fmaf(lb - pl, lz.invp, tt), lz.te[j]);
+        if (lz.te[j] <= tt) {  // opU in table order, later entries win ties
+          const float v = prim_dist<true>(S.entry(j), S.type(j), p, S.blend, S.omblend);
+          idp = (v <= m) ? j : idp;
+          m = vmin(m, v);
+        }
+      }
+      lz.temin = slot_min(lz.te, ns);
+      lz.idb = idp;
+    }
+    return m;
+  };
+  float tp = t;
+  auto run = [&](auto esc, auto useT) {
+    for (int i = i0;; ++i) {
+      const float d = step(t);
+      bool e = d < 0.000001f * t;
+      dl = d;
+      tp = t;
+      t = t + d;
+      if (decltype(useT)::value) e = e | !(t <= T);
+      if (decltype(esc)::value) e = e | (d > tmax);
+      if (e | (i >= nmax)) break;
+    }
+    t = tp;
+  };
+  const bool useT = wany(!(T == __builtin_huge_valf()));
+  if (__all(S.no_escape(ro, rd, tmax))) {
+    if (useT) run(No(), Yes());
+    else run(No(), No());
+  } else {
+    if (useT) run(Yes(), Yes());
+    else run(Yes(), No());
+  }
+  if (dl < 0.000001f * t) {
+    // the winner: the plane (last in opU order, it wins a tie) exactly when the
+    // hit step's distance is its value; otherwise the block ran at this step and
+    // idb is its winner (lazy_id, rm_scene.hpp)
+    const f3 p = add(ro, muls(rd, t));
+    const int k = dl != plane(p.y) ? lz.idb : kp;
+    return THit{t, S.id(k), S.material(k), S.color(k, p), dl};
+  }
+  return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
+}
+#endif
+
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161
 template <bool COUNT, int KL>
 __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c,
                                    const float* prep = nullptr) {
+#ifdef RM_TABLE_STATIC
+  if (!COUNT && slazy_table(S)) return smarch<KL>(S, ro, rd, reflected, prep);
+#endif
   // ro in VGPRs (a primary ray's ro is the camera, uniform): every step's p(t)
   // then pairs for dual issue instead of taking a whole slot per component, and
   // the generic kernel spills less (28 -> 12 B of scratch per lane): -2.9 % per

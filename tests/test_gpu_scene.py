@@ -250,6 +250,53 @@ def test_specialised_tables_equal_generic(rm, gpu, seed, nplanes):
               _render(rm, u, 96, 64, scene=scene, counters=counters))
 
 
+def floor_last_scene(rm, seed):
+    """A reference-shaped table (the specialised kernel's built-in-style march,
+    rm_table.hip smarch): random bounded entries, then one axis-aligned floor
+    plane q.y n_y + w as the last entry, n_y of either sign and not unit."""
+    g = np.random.default_rng(1000 + seed)
+    prims = random_scene(rm, seed, nplanes=0)[:7]  # every bounded entry in a lazy slot (<= 8)
+    ny = float(g.choice([1.0, 0.5, 2.0, -1.0]))  # -1: a ceiling above the scene
+    w = float(g.uniform(4, 7)) * abs(ny)
+    prims.append(rm.primitive(rm.PRIM_PLANE, (0.0, 0.0, 0.0), (0.0, ny, 0.0, w), (0.5, 0.5, 0.5),
+                              id=7, material=0.0, paint=1))
+    return prims
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_specialised_floor_tables_equal_generic(rm, gpu, seed):
+    """Reference-shaped tables take the specialised kernels' lazy block (plane
+    budget, slack line, bounded sqrt form): the same image, counters and sdf
+    counts as the generic kernel."""
+    scene = floor_last_scene(rm, seed)
+    f, b, aa, sm = [(10, 2, True, 0), (60, 3, False, 0), (100, 5, True, 1)][seed % 3]
+    u = rm.sweep_uniforms(f, 120, b, aa, sm)
+    for counters in (True, False):
+        _same(_render_spec(rm, u, 96, 64, scene, counters=counters),
+              _render(rm, u, 96, 64, scene=scene, counters=counters))
+
+
+def test_specialised_far_camera_uses_generic(rm, gpu):
+    """A camera farther than 1e15 from the origin is outside the specialised
+    kernels' bounded-point assumption (rm_api.hip frame_jit): the frame renders
+    with the generic kernel, and graph replay re-captures both ways."""
+    near = rm.sweep_uniforms(60, 120, 3, True, 0)
+    far = rm.sweep_uniforms(60, 120, 3, True, 0)
+    far.camera.pos[0] = 3e15
+    want = {k: _render(rm, u, 64, 48, scene=rm.default_scene(), counters=False)["rgba32f"]
+            for k, u in (("near", near), ("far", far))}
+    with rm.Renderer(64, 48, outputs=OUT) as r:
+        r.specialize_scene(True)
+        r.set_scene(rm.default_scene())
+        for k, u in (("near", near), ("far", far), ("near", near)):
+            r.dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba32f(), want[k])
+        r.graph_enable(True)
+        for k, u in (("far", far), ("near", near), ("far", far)):
+            r.graph_dispatch(u)
+            np.testing.assert_array_equal(r.read_rgba32f(), want[k])
+
+
 def test_specialise_toggle_and_graph(rm, gpu):
     """Toggling specialisation and switching tables re-captures the graph."""
     a, b = rm.default_scene(), random_scene(rm, 7)
