@@ -281,7 +281,10 @@ int rm_get_scene(const rm_ctx *ctx, rm_primitive *out, int32_t capacity, int32_t
  * CreateCompute shader.hpp:186-197).  Same image as the generic table kernel;
  * compiles are cached per process and device.  A failed compile returns
  * RM_ERR_HIP with the compiler log in rm_last_error and leaves the scene as it
- * was.  enable == 0: the generic (LDS-staged) table kernel. */
+ * was.  A frame whose camera lies farther than 1e15 from the origin (or is not
+ * finite) renders with the generic kernel: the specialised kernels take an
+ * exact short form of sqrt(x) - R that needs bounded march points.
+ * enable == 0: the generic (LDS-staged) table kernel. */
 int rm_scene_specialize(rm_ctx *ctx, int enable);
 /* The register bound of the specialised table kernels in use: *waves = the
  * waves per SIMD they were compiled for (8, 7 or 6: the most at which they need
