@@ -23,7 +23,8 @@
 namespace rm {
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
-hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots);
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy);
+bool table_slazy(const uint32_t* words, int32_t n);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
 hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
@@ -412,10 +413,15 @@ static int table_slots(const rm_ctx* c) {
   const float* ex = reinterpret_cast<const float*>(c->scene_words.data()) + (size_t)c->nprims * rm::TABLE_WORDS;
   return (int)ex[rm::EX_NSLOTS];
 }
+// A reference-shaped table (rm_table.hip table_slazy): the generic kernel's
+// production instance with the built-in march shape.
+static bool table_sl(const rm_ctx* c) {
+  return c->nprims && table_slots(c) <= rm::TABLE_FEW_SLOTS && rm::table_slazy(c->scene_words.data(), c->nprims);
+}
 // Which kernel a frame renders with (the graph's key): 0 built-in, 1 + the
-// generic table kernel's slot instance.
+// generic table kernel's instance (slots, shape).
 static int table_key(const rm_ctx* c) {
-  return c->nprims ? 1 + (table_slots(c) <= rm::TABLE_FEW_SLOTS ? 0 : 1) : 0;
+  return c->nprims ? 1 + (table_slots(c) <= rm::TABLE_FEW_SLOTS ? 0 : 1) + (table_sl(c) ? 2 : 0) : 0;
 }
 
 void table_prep_host(const uint32_t* words, int32_t n, const float cam[3], float blend, float omblend,
@@ -1128,7 +1134,7 @@ int render_launch(rm_ctx* c) {
   // a runtime scene table renders with the table kernel
   const rm::JitTable* jit = frame_jit(c, F);
   hipError_t e = c->nprims ? (jit ? rm::launch_table_jit(jit, F, c->cfg.counters != 0, c->stream)
-                                  : rm::launch_table(F, c->cfg.counters != 0, c->stream, table_slots(c)))
+                                  : rm::launch_table(F, c->cfg.counters != 0, c->stream, table_slots(c), table_sl(c)))
                            : rm::launch_pixel(F, c->cfg.counters != 0, c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
   if (e1) RM_HIP(c, hipEventRecord(e1, c->stream));
@@ -1243,7 +1249,7 @@ int launch_batch(rm_ctx* c, const rm_uniforms* u, int n, O8 out8, O32 out32) {
     if (c->nprims) {
       const rm::JitTable* jit = frame_jit(c, F);
       const hipError_t e = jit ? rm::launch_table_jit(jit, F, false, c->stream)
-                               : rm::launch_table(F, false, c->stream, table_slots(c));
+                               : rm::launch_table(F, false, c->stream, table_slots(c), table_sl(c));
       if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
       continue;
     }
@@ -1606,7 +1612,7 @@ static int graph_capture(rm_ctx* c, const rmd::Frame& F) {
   if (e == hipSuccess) {
     e = !F.nprims ? rm::launch_pixel(F, false, cs)
         : frame_jit(c, F) ? rm::launch_table_jit(frame_jit(c, F), F, false, cs)
-                  : rm::launch_table(F, false, cs, table_slots(c));
+                  : rm::launch_table(F, false, cs, table_slots(c), table_sl(c));
     // the render node: the one node the next captured operation would depend on
     hipStreamCaptureStatus st;
     const hipGraphNode_t* deps = nullptr;

@@ -33,6 +33,9 @@
 #endif
 
 #include "rm_internal.hpp"
+#ifndef __HIPCC_RTC__
+#include <cstring>
+#endif
 #include "rm_scene.hpp"
 
 // RM_TABLE_STATIC: this file compiled at rm_set_scene time by hiprtc
@@ -530,17 +533,19 @@ struct THit {
   float d;  // a hit's last distance: sdf at the hit point itself (GetNormal's centre sample)
 };
 
-#ifdef RM_TABLE_STATIC
 // ---- the built-in kernel's march shape for reference-shaped tables -------------
-// A specialised table whose bounded entries all sit in lazy slots and whose one
-// plane is its last entry, axis-aligned (q.y n_y + w, as the reference's floor):
-// the production march then runs scene_lazy's block (rm_scene.hpp) over the
-// table instead of TLazy.  Per step only p.y and the plane value; the block is
+// A table whose bounded entries all sit in lazy slots and whose one plane is its
+// last entry, axis-aligned (q.y n_y + w, as the reference's floor): the
+// production march then runs scene_lazy's block (rm_scene.hpp) over the table
+// instead of TLazy -- in the specialised kernels (the table folded in), and in
+// the generic kernel's reference-shaped instances (SL, chosen on the host:
+// rm::table_slazy; one march per instance keeps its registers as they were).  Per step only p.y and the plane value; the block is
 // entered when some lane's expiry passes t, forms p.x / p.z, the slack from a
 // line in t and re-tests the due slots in table order, evaluating an entry
 // exactly where its new expiry does not pass t.  Same values, fewer
 // instructions: the culling only skips entries proven strictly above the
 // minimum, as TLazy's.
+#ifdef RM_TABLE_STATIC
 __device__ __forceinline__ bool slazy_table(const Table& S) {
   const float* ex = S.exits();
   const int kp = S.n - 1;
@@ -554,6 +559,7 @@ __device__ __forceinline__ bool slazy_table(const Table& S) {
     if ((int)ex[rm::EX_SLOTS + j] != j) return false;  // ... slot j holding entry j
   return true;
 }
+#endif
 
 // Expiries by TLazy's argument (above), in scene_lazy's form:
 //   * the slack is the line s0 + s1 t >= TLazy's sl(p(t)): |p|_1 <= (|ro|_1 +
@@ -596,9 +602,14 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   const float tmax = reflected ? 200.0f : 400.0f;
   const int nmax = reflected ? 256 : 512;
   const float T = table_exit_T(ex, MISS_C, 0.0f, ro, rd);
+  // the plane's value at height y, prim_dist's float operations (q.x, q.z unused;
+  // the generic kernel's fast plane is the same arithmetic on staged registers)
+#ifdef RM_TABLE_STATIC
   const float* PL = S.entry(kp);
-  // the plane's value at height y, prim_dist's float operations (q.x, q.z unused)
   auto plane = [&](float y) { return prim_dist(PL, RM_PRIM_PLANE, mk(0.0f, y, 0.0f), S.blend, S.omblend); };
+#else
+  auto plane = [&](float y) { return S.plane_fast(mk(0.0f, y, 0.0f)); };
+#endif
   SLazy<KL> lz;
   {
     const float sig2 = 2.0f * ex[rm::EX_SIGMA];
@@ -645,14 +656,19 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
       RM_TS_UNROLL
       for (int j = 0; j < KL; ++j) {
         if (j >= ns || !wany(tt >= lz.te[j])) continue;
+#ifdef RM_TABLE_STATIC
         const float* B = S.entry(j) + rm::TW_BALL;
+#else
+        const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];  // the slot's ball, staged
+        const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+#endif
         const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
                                         1.0f - 0x1p-12f, -B[3]);
         // (the plane budget alone, as scene_lazy's re-test: rm_scene.hpp)
         lz.te[j] = vmax(__builtin_fmaf(lb - pl, lz.invp, tt), lz.te[j]);
         if (lz.te[j] <= tt) {  // opU in table order, later entries win ties
-          const float v = prim_dist<true>(S.entry(j), S.type(j), p, S.blend, S.omblend);
+          const float v = prim_dist<kBoundedPoints>(S.entry(j), S.type(j), p, S.blend, S.omblend);
           idp = (v <= m) ? j : idp;
           m = vmin(m, v);
         }
@@ -694,14 +710,15 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   }
   return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
 }
-#endif
 
 // RayMarch glsl:125-142 / reflectedRay glsl:144-161
-template <bool COUNT, int KL>
+template <bool COUNT, int KL, bool SL = false>
 __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c,
                                    const float* prep = nullptr) {
 #ifdef RM_TABLE_STATIC
   if (!COUNT && slazy_table(S)) return smarch<KL>(S, ro, rd, reflected, prep);
+#else
+  if (!COUNT && SL) return smarch<KL>(S, ro, rd, reflected, prep);
 #endif
   // ro in VGPRs (a primary ray's ro is the camera, uniform): every step's p(t)
   // then pairs for dual issue instead of taking a whole slot per component, and
@@ -851,7 +868,7 @@ __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 
 
 // bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
 // the colour unchanged (glsl:181, 189-190): the loop stops there.
-template <bool COUNT, int KL>
+template <bool COUNT, int KL, bool SL = false>
 __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 normal, f3 color,
                       const THit& primary, TCnt& c) {
   float prevMat = primary.material;
@@ -860,10 +877,10 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
   for (int i = 1; i <= F.bounces; ++i) {
     if (prevMat == 0.0f) break;
     rayDir = reflect(rayDir, normal);
-    THit h = tmarch<COUNT, KL>(S, add(pos, muls(normal, 0.001f)), rayDir, true, c);
+    THit h = tmarch<COUNT, KL, SL>(S, add(pos, muls(normal, 0.001f)), rayDir, true, c);
 #ifdef RM_TDBL_BMARCH
     if (!COUNT) {
-      const THit h2 = tmarch<COUNT, KL>(S, topaque(add(pos, muls(normal, 0.001f))), rayDir, true, c);
+      const THit h2 = tmarch<COUNT, KL, SL>(S, topaque(add(pos, muls(normal, 0.001f))), rayDir, true, c);
       h.t = (h2.t == h.t) ? h.t : __builtin_nanf("");
     }
 #endif
@@ -900,13 +917,13 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
 }
 
 // render glsl:218-251
-template <bool COUNT, int KL>
+template <bool COUNT, int KL, bool SL = false>
 __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
-  THit h = tmarch<COUNT, KL>(S, ro, rd, false, c, F.prepv);
+  THit h = tmarch<COUNT, KL, SL>(S, ro, rd, false, c, F.prepv);
 #ifdef RM_TDBL_MARCH
   if (!COUNT) {
-    const THit h2 = tmarch<COUNT, KL>(S, topaque(ro), rd, false, c, F.prepv);
+    const THit h2 = tmarch<COUNT, KL, SL>(S, topaque(ro), rd, false, c, F.prepv);
     h.t = (h2.t == h.t) ? h.t : __builtin_nanf("");
   }
 #endif
@@ -929,7 +946,7 @@ __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd,
 #endif
       return gamma(muls(color, sh));
     }
-    if (F.bounces > 0) color = tbounce<COUNT, KL>(F, S, rd, pos, normal, color, h, c);
+    if (F.bounces > 0) color = tbounce<COUNT, KL, SL>(F, S, rd, pos, normal, color, h, c);
   }
   return gamma(color);
 }
@@ -996,7 +1013,7 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 #endif
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS>
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
 __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
@@ -1016,7 +1033,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F)
   f3 ro, rd;
   cast_ray(F, lane_uv(F, 0, px, -1), lane_uv(F, 1, py, -1), ro, rd);
   if (COUNT) c.rays++;
-  const f3 col = trender<COUNT, KL>(F, S, ro, rd, c);
+  const f3 col = trender<COUNT, KL, SL>(F, S, ro, rd, c);
   store_pixel(F, idx, col.x, col.y, col.z, 1.0f);
   if (COUNT) {
     F.sdf_counts[idx] = c.march + c.reflect + c.shadow + 4u * c.normals;
@@ -1027,7 +1044,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F)
 // main glsl:291-344 with 4x supersampling: one lane per (pixel, sample), the 4
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS>
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
 __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
@@ -1045,7 +1062,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F
     f3 ro, rd;
     cast_ray(F, lane_uv(F, 0, px, s), lane_uv(F, 1, py, s), ro, rd);
     if (COUNT) c.rays++;
-    col = trender<COUNT, KL>(F, S, ro, rd, c);
+    col = trender<COUNT, KL, SL>(F, S, ro, rd, c);
   }
   const float r1 = __shfl(col.x, lane + 1), g1 = __shfl(col.y, lane + 1), b1 = __shfl(col.z, lane + 1);
   const float r2 = __shfl(col.x, lane + 2), g2 = __shfl(col.y, lane + 2), b2 = __shfl(col.z, lane + 2);
@@ -1073,7 +1090,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F
 namespace rm {
 
 namespace {
-template <int KL>
+template <int KL, bool SL>
 void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
   // the table, then the lazy slots' balls (Table::sb)
   const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
@@ -1082,13 +1099,13 @@ void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
     if (counters)
       hipLaunchKernelGGL((rmd::k_table_sample<true, KL>), g, dim3(64), lds, s, F);
     else
-      hipLaunchKernelGGL((rmd::k_table_sample<false, KL>), g, dim3(64), lds, s, F);
+      hipLaunchKernelGGL((rmd::k_table_sample<false, KL, SL>), g, dim3(64), lds, s, F);
   } else {
     const dim3 g((F.width + 7) / 8, (F.rows + 7) / 8);
     if (counters)
       hipLaunchKernelGGL((rmd::k_table_pixel<true, KL>), g, dim3(64), lds, s, F);
     else
-      hipLaunchKernelGGL((rmd::k_table_pixel<false, KL>), g, dim3(64), lds, s, F);
+      hipLaunchKernelGGL((rmd::k_table_pixel<false, KL, SL>), g, dim3(64), lds, s, F);
   }
 }
 }  // namespace
@@ -1097,10 +1114,35 @@ void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
 // at most TABLE_FEW_SLOTS of them (the reference scene has 5) take an instance
 // holding that many: 3 fewer live expiries in the march loops, 15 -> 8 spilled
 // VGPRs at the 7-wave bound, -2.4 % per cfg3 frame.
-hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots) {
-  if (nslots <= TABLE_FEW_SLOTS) launch_table_kl<TABLE_FEW_SLOTS>(F, counters, s);
-  else launch_table_kl<rm::EX_MAX_SLOTS>(F, counters, s);
+// slazy: the table is reference-shaped (table_slazy): the production kernels
+// of the few-slot instance take the built-in march shape (smarch); the counting
+// kernels keep TLazy.  (An 8-slot smarch instance spills 43 VGPRs at the 7-wave
+// bound: larger tables keep TLazy.)
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy) {
+  if (nslots <= TABLE_FEW_SLOTS) {
+    if (slazy) launch_table_kl<TABLE_FEW_SLOTS, true>(F, counters, s);
+    else launch_table_kl<TABLE_FEW_SLOTS, false>(F, counters, s);
+  } else {
+    launch_table_kl<rm::EX_MAX_SLOTS, false>(F, counters, s);
+  }
   return hipGetLastError();
+}
+
+// smarch's conditions on a compiled table (slazy_table, device): valid exit
+// bounds; exactly one plane, the last entry, unswizzled, normal (0, n_y, 0);
+// every other entry in a lazy slot, slot j holding entry j.
+bool table_slazy(const uint32_t* words, int32_t n) {
+  const float* t = reinterpret_cast<const float*>(words);
+  const float* ex = t + (size_t)n * TABLE_WORDS;
+  const float* P = t + (size_t)(n - 1) * TABLE_WORDS;
+  int type, swz;
+  std::memcpy(&type, P + TW_TYPE, sizeof type);
+  std::memcpy(&swz, P + TW_SWIZZLE, sizeof swz);
+  if (ex[EX_VALID] == 0.0f || ex[EX_NPLANES] != 1.0f || type != RM_PRIM_PLANE || swz != RM_SWIZZLE_XYZ) return false;
+  if (!(P[TW_P] == 0.0f && P[TW_P + 2] == 0.0f) || (int)ex[EX_NSLOTS] != n - 1) return false;
+  for (int j = 0; j < n - 1; ++j)
+    if ((int)ex[EX_SLOTS + j] != j) return false;
+  return true;
 }
 
 }  // namespace rm
