@@ -581,15 +581,20 @@ struct SLazy {
   int idb;  // the entry the last block's values made the winner (the plane: n - 1)
 };
 
-// The minimum over the first ns expiries (ns a compile-time count), three at a
-// time (v_min3_f32).
+// The minimum over the expiries, three at a time (v_min3_f32): the first ns
+// (a compile-time count) in a specialised kernel; all KL in the generic one,
+// whose unused slots hold +inf (a runtime bound would index the array, which
+// then lives in scratch).
 template <int KL>
 __device__ __forceinline__ float slot_min(const float (&te)[KL], int ns) {
+#ifndef RM_TABLE_STATIC
+  ns = KL;
+#endif
   float m = te[0];
   int j = 1;
-  RM_TS_UNROLL
+  #pragma unroll
   for (; j + 1 < KL && j + 1 < ns; j += 2) m = vmin3(m, te[j], te[j + 1]);
-  RM_TS_UNROLL
+  #pragma unroll
   for (; j < KL && j < ns; ++j) m = vmin(m, te[j]);
   return m;
 }
@@ -632,13 +637,13 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   if (prep && prep[rm::TP_VALID] != 0.0f) {
     // step 0 at the camera, evaluated on the host (tmarch above); the gaps are
     // TLazy's, their expiries at TLazy's rate
-    RM_TS_UNROLL
+    #pragma unroll
     for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f) : __builtin_huge_valf();
     dl = prep[rm::TP_D0];
     t = dl;
     i0 = 2;
   } else {
-    RM_TS_UNROLL
+    #pragma unroll
     for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? NEG : __builtin_huge_valf();
   }
   lz.temin = slot_min(lz.te, ns);
@@ -653,7 +658,7 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
       const float pl = m + sl;
       const f3 p = mk(ro.x + rd.x * tt, py, ro.z + rd.z * tt);
       int idp = kp;
-      RM_TS_UNROLL
+      #pragma unroll
       for (int j = 0; j < KL; ++j) {
         if (j >= ns || !wany(tt >= lz.te[j])) continue;
 #ifdef RM_TABLE_STATIC
@@ -1011,10 +1016,15 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 #ifndef RM_TABLE_MIN_WAVES
 #define RM_TABLE_MIN_WAVES 7
 #endif
+// The reference-shaped instance (SL): 7 waves, 7 spilled VGPRs (32 B per lane),
+// -4.5 % per cfg3 frame against 6 waves (80 VGPRs, no scratch), round 4.
+#ifndef RM_TABLE_SL_WAVES
+#define RM_TABLE_SL_WAVES 7
+#endif
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
 template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
-__global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
   const int lane = threadIdx.x;
@@ -1045,7 +1055,7 @@ __global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F)
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
 template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
-__global__ __launch_bounds__(64, RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
   extern __shared__ float lds[];
   const Table S = stage(F, lds);
   const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
