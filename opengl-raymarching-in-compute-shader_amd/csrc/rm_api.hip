@@ -416,7 +416,7 @@ static int table_slots(const rm_ctx* c) {
 // A reference-shaped table (rm_table.hip table_slazy): the generic kernel's
 // production instance with the built-in march shape.
 static bool table_sl(const rm_ctx* c) {
-  return c->nprims && table_slots(c) <= rm::TABLE_FEW_SLOTS && rm::table_slazy(c->scene_words.data(), c->nprims);
+  return c->nprims && rm::table_slazy(c->scene_words.data(), c->nprims);
 }
 // Which kernel a frame renders with (the graph's key): 0 built-in, 1 + the
 // generic table kernel's instance (slots, shape).

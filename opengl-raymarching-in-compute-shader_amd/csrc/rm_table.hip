@@ -1125,15 +1125,14 @@ void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
 // holding that many: 3 fewer live expiries in the march loops, 15 -> 8 spilled
 // VGPRs at the 7-wave bound, -2.4 % per cfg3 frame.
 // slazy: the table is reference-shaped (table_slazy): the production kernels
-// of the few-slot instance take the built-in march shape (smarch); the counting
-// kernels keep TLazy.  (An 8-slot smarch instance spills 43 VGPRs at the 7-wave
-// bound: larger tables keep TLazy.)
+// take the built-in march shape (smarch); the counting kernels keep TLazy.
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy) {
   if (nslots <= TABLE_FEW_SLOTS) {
     if (slazy) launch_table_kl<TABLE_FEW_SLOTS, true>(F, counters, s);
     else launch_table_kl<TABLE_FEW_SLOTS, false>(F, counters, s);
   } else {
-    launch_table_kl<rm::EX_MAX_SLOTS, false>(F, counters, s);
+    if (slazy) launch_table_kl<rm::EX_MAX_SLOTS, true>(F, counters, s);
+    else launch_table_kl<rm::EX_MAX_SLOTS, false>(F, counters, s);
   }
   return hipGetLastError();
 }

@@ -255,7 +255,8 @@ def floor_last_scene(rm, seed):
     rm_table.hip smarch): random bounded entries, then one axis-aligned floor
     plane q.y n_y + w as the last entry, n_y of either sign and not unit."""
     g = np.random.default_rng(1000 + seed)
-    prims = random_scene(rm, seed, nplanes=0)[:7]  # every bounded entry in a lazy slot (<= 8)
+    # 3..7 bounded entries (every one in a lazy slot): the 5- and 8-slot instances
+    prims = random_scene(rm, seed, nplanes=0)[:3 + seed % 5]
     ny = float(g.choice([1.0, 0.5, 2.0, -1.0]))  # -1: a ceiling above the scene
     w = float(g.uniform(4, 7)) * abs(ny)
     prims.append(rm.primitive(rm.PRIM_PLANE, (0.0, 0.0, 0.0), (0.0, ny, 0.0, w), (0.5, 0.5, 0.5),
@@ -274,6 +275,23 @@ def test_specialised_floor_tables_equal_generic(rm, gpu, seed):
     for counters in (True, False):
         _same(_render_spec(rm, u, 96, 64, scene, counters=counters),
               _render(rm, u, 96, 64, scene=scene, counters=counters))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_floor_tables_match_oracle(rm, oracle, gpu, seed):
+    """Reference-shaped tables through the generic kernel: the counting kernel
+    (TLazy) against the oracle's table mode, and the production kernel's
+    reference-shaped instance (smarch, 5 or 8 slots) against the counting image
+    bit for bit."""
+    scene = floor_last_scene(rm, seed)
+    f, b, aa, sm = [(10, 2, True, 0), (60, 3, False, 0), (100, 5, True, 1), (30, 1, False, 0)][seed % 4]
+    u = rm.sweep_uniforms(f, 120, b, aa, sm)
+    W, H = 96, 64
+    ref = oracle.render(u, W, H, scene=scene)
+    got = _render(rm, u, W, H, scene=scene)
+    _compare(ref, got, f"floor seed {seed}")
+    prod = _render(rm, u, W, H, scene=scene, counters=False)
+    np.testing.assert_array_equal(prod["rgba32f"], got["rgba32f"])
 
 
 def test_specialised_far_camera_uses_generic(rm, gpu):

@@ -2,6 +2,9 @@
 
   python tools/ab_kernel.py [--cfg 3] [--rounds 4] [--frames 30] [--table] [--spec] [variant.so ...]
 
+RM_AB_WIDE=1 with --table / --spec: the reference scene with two more spheres
+before its floor (7 bounded entries: the tables' 8-slot instances).
+
 --batch B --ctx N times throughput instead: the frames as rm_dispatch_frames
 batches of B over N contexts (wall time per frame, after a 0.3 s spin-up).
 
@@ -64,7 +67,18 @@ def child(cfg, frames, table, spec=False):
         if spec:
             r.specialize_scene(True)
         if table or spec:
-            r.set_scene(rm.default_scene())
+            sc = rm.default_scene()
+            if os.environ.get("RM_AB_WIDE") == "1":
+                # 7 bounded entries and the floor last: the 8-slot instances
+                import ctypes as C
+                extra = []
+                for dx in (40.0, -40.0):
+                    q = rm.rm_primitive()
+                    C.memmove(C.byref(q), C.byref(sc[0]), C.sizeof(q))
+                    q.center[0] += dx
+                    extra.append(q)
+                sc = sc[:-1] + extra + sc[-1:]
+            r.set_scene(sc)
         r.enable_timing(True)
         for f in range(3):
             r.dispatch(rm.sweep_uniforms(f, 120, b, aa, sm))
