@@ -210,13 +210,17 @@ def default_batch(config: int, dist_on: bool, one_comm: bool, steps: int) -> int
     frames per launch on 3 contexts render at 0.0090 / 0.0575 ms per frame against
     0.0124 / 0.0594 for 10 on 2 (round 4, tools/probe_batch.py --steps 120,
     profiles/r04_probe_batch120.txt); fewer steps cap the batch so that the launches
-    still spread over the 3 contexts.  The 4K / 8K supersampled frames fill the chip
-    by themselves; 3 frames in flight and batches measure the same there."""
+    still spread over the 3 contexts.  The 4K supersampled frames fill the chip by
+    themselves: pairs of frames on 4 contexts measure 0.8 % faster than single frames
+    on 3 (0.8193 against 0.8258 ms, 7 interleaved rounds, profiles/r04_inflight.txt);
+    the 8K graph-replayed frames (cfg5) stay single, 3 in flight."""
     if one_comm:
         return 4  # N > 1, one communicator: gather batch j while batch j + 1 renders
     if dist_on:
         return 1
-    return max(1, min(20, -(-steps // 3))) if config in (1, 2) else 1
+    if config in (1, 2):
+        return max(1, min(20, -(-steps // 3)))
+    return 2 if config in (3, 4) else 1
 
 
 def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
@@ -362,8 +366,9 @@ def main() -> int:
     one_comm = dist_on and args.comms == 1
     batch = args.batch if args.batch > 0 else default_batch(args.config, dist_on, one_comm, args.steps)
     batch = max(1, min(batch, rm.RM_MAX_BATCH, args.steps))
-    # contexts in flight: 3 frames or batches on one GPU, 4 frames of a sharded step
-    nfl = args.inflight if args.inflight > 0 else (3 if not dist_on else 4)
+    # contexts in flight: 3 frames or batches on one GPU (4 for the 4K pairs), 4
+    # frames of a sharded step
+    nfl = args.inflight if args.inflight > 0 else (4 if dist_on or (batch == 2 and args.config in (3, 4)) else 3)
     nfl = nfl if (not dist_on or args.pipeline) else 1
     if one_comm:
         nfl = 1  # one context, one communicator; batches overlap through its gather stream
