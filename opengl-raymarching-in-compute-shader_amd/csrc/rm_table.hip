@@ -539,12 +539,12 @@ struct THit {
 // production march then runs scene_lazy's block (rm_scene.hpp) over the table
 // instead of TLazy -- in the specialised kernels (the table folded in), and in
 // the generic kernel's reference-shaped instances (SL, chosen on the host:
-// rm::table_slazy; one march per instance keeps its registers as they were).  Per step only p.y and the plane value; the block is
-// entered when some lane's expiry passes t, forms p.x / p.z, the slack from a
-// line in t and re-tests the due slots in table order, evaluating an entry
-// exactly where its new expiry does not pass t.  Same values, fewer
-// instructions: the culling only skips entries proven strictly above the
-// minimum, as TLazy's.
+// rm::table_slazy; one march per instance keeps its registers as they were).
+// Per step only p.y and the plane value; the block is entered when some lane's
+// expiry passes t, forms p.x / p.z, the slack from a line in t and re-tests the
+// due slots in table order, evaluating an entry exactly where its new expiry
+// does not pass t.  Same values, fewer instructions: the culling only skips
+// entries proven strictly above the minimum, as TLazy's.
 #ifdef RM_TABLE_STATIC
 __device__ __forceinline__ bool slazy_table(const Table& S) {
   const float* ex = S.exits();
