@@ -202,6 +202,16 @@ int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::
   code.clear();
   std::vector<char> c;
   std::vector<std::string> l;
+  if (const char* fw = std::getenv("RM_JIT_FORCE_WAVES"); fw && *fw) {
+    // diagnostic A/Bs only: this bound whatever scratch it costs
+    const int wf = std::atoi(fw);
+    const int rf = jit_compile_waves(words, n, arch, wf, c, l, err);
+    if (rf != RM_OK) return rf;
+    code.swap(c);
+    lowered.swap(l);
+    if (waves) *waves = wf;
+    return RM_OK;
+  }
   int rc = jit_compile_waves(words, n, arch, 1, c, l, err);
   if (rc != RM_OK) return rc;
   int w = production_waves(c, l, err);
