@@ -9,20 +9,21 @@
 // arithmetic is the same source under the same flags (-ffp-contract=off), so the
 // image equals the generic table kernel's bit for bit (tests/test_gpu_scene.py).
 //
-// Register bound per table: the kernels run at the most waves per SIMD (8, 7 or
-// 6) at which the production kernels need no scratch (private segment 0 in their
-// kernel descriptors).  One compile usually decides it (round 4, VERDICT r03
-// #6): the table is compiled without an occupancy bound (RM_TABLE_MIN_WAVES = 1),
-// the descriptors give each production kernel's VGPR allocation, and a kernel
-// that allocates at most 512 / w registers already runs at w waves with no
-// scratch.  The reference scene's kernels allocate 72 VGPRs unbounded: 7 waves,
-// the bound the round-2 ladder (8, then 7) found with two compiles; bounded to 8
-// waves they spill.  Only a table whose kernels need more than 80 registers
-// unbounded is compiled once more, bounded to 6 waves, and that build is kept
-// if it needs no scratch; one that spills even there (a 30-entry table spills
-// 100+ VGPRs at 4 waves) is not specialised and renders with the generic
-// (LDS-staged) kernel, whose registers do not grow with the table.  RM_JIT_LOG=1
-// prints one line per hiprtc compile (stderr).
+// Register bound per table.  First compile: bounded to 8 waves per SIMD, kept
+// when the production kernels spill at most kFewSpillBytes of scratch per lane
+// (their kernel descriptors' private segment).  The reference scene's kernels
+// spill 7 VGPRs there (32 B) and render a cfg3 frame 1.8 % faster than at the
+// spill-free 7-wave bound (round 4, profiles/r04_spec_waves.txt); a table whose
+// kernels fit 64 registers compiles the same as without a bound.  Otherwise the
+// spill-free ladder: a compile without an occupancy bound (RM_TABLE_MIN_WAVES =
+// 1), whose descriptors give each production kernel's VGPR allocation (a kernel
+// allocating at most 512 / w registers runs at w waves with no scratch), and
+// only for a table needing more than 80 registers one more, bounded to 6 waves,
+// kept if it needs no scratch; one that spills even there (a 30-entry table
+// spills 100+ VGPRs at 4 waves) is not specialised and renders with the generic
+// (LDS-staged) kernel, whose registers do not grow with the table.  The
+// reference scene compiles once.  RM_JIT_LOG=1 prints one line
+// per hiprtc compile (stderr).
 //
 // Modules are cached per (device, table words) for the life of the process:
 // contexts rendering the same table (frames in flight) share one compile.
@@ -191,11 +192,26 @@ int production_waves(const std::vector<char>& c, const std::vector<std::string>&
   return w;
 }
 
-// The table kernels at the most waves per SIMD (8, 7, 6) whose production
-// kernels use no scratch: *waves is that, or 0 (code left empty) when none
-// fits.  One compile without an occupancy bound decides every table whose
-// kernels fit 80 registers (above); a second, bounded to 6 waves, runs only for
-// a larger one.
+// The largest scratch bytes per lane of the production kernels, or -1 (with
+// err) when a descriptor is missing.
+long production_scratch(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
+  long most = 0;
+  for (int k : {0, 2}) {
+    long priv = -1;
+    int vg = 0;
+    if (!kernel_desc(c, l[k], &priv, &vg)) {
+      err = "rm_scene_specialize: kernel descriptor " + l[k] + ".kd not found in the compiled code object";
+      return -1;
+    }
+    most = priv > most ? priv : most;
+  }
+  return most;
+}
+
+constexpr long kFewSpillBytes = 32;  // 8 spilled VGPRs per lane
+
+// The table kernels at their register bound (above): *waves is the waves per
+// SIMD they run at, or 0 (code left empty) when no bound fits.
 int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::vector<char>& code,
                 std::vector<std::string>& lowered, std::string& err, int* waves) {
   if (waves) *waves = 0;
@@ -212,7 +228,17 @@ int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::
     if (waves) *waves = wf;
     return RM_OK;
   }
-  int rc = jit_compile_waves(words, n, arch, 1, c, l, err);
+  int rc = jit_compile_waves(words, n, arch, 8, c, l, err);
+  if (rc != RM_OK) return rc;
+  const long sc = production_scratch(c, l, err);
+  if (sc < 0) return RM_ERR_HIP;
+  if (sc <= kFewSpillBytes) {
+    code.swap(c);
+    lowered.swap(l);
+    if (waves) *waves = 8;
+    return RM_OK;
+  }
+  rc = jit_compile_waves(words, n, arch, 1, c, l, err);
   if (rc != RM_OK) return rc;
   int w = production_waves(c, l, err);
   if (w < 0) return RM_ERR_HIP;

@@ -119,16 +119,17 @@ def _kernel_private_sizes(co):
 def test_table_specialises_without_a_device(rm):
     """rm_scene_specialize's hiprtc compile (rm_jit.hip) runs here, without a GPU:
     the embedded rm_table.hip compiles for gfx950 with the table folded in, and
-    the code object holds the four table kernels.  The register bound is the most
-    waves per SIMD at which the production kernels need no scratch:
-    their kernel descriptors carry a zero private segment."""
+    the code object holds the four table kernels.  The register bound (ADVICE r01,
+    round 4): 8 waves per SIMD when the production kernels spill at most 32 B of
+    scratch per lane there, as the reference scene's do, else the most waves at
+    which they need none; the kernel descriptors carry the private segment."""
     rc, co = _code_object(rm, rm.default_scene())
     assert rc == 0 and co[:4] == b"\x7fELF"
     for name in (b"k_table_pixelILb0E", b"k_table_pixelILb1E", b"k_table_sampleILb0E", b"k_table_sampleILb1E"):
         assert name in co
     priv = _kernel_private_sizes(co)
     prod = {k: v for k, v in priv.items() if "ILb0E" in k}
-    assert len(prod) == 2 and all(v == 0 for v in prod.values()), priv
+    assert len(prod) == 2 and all(v <= 32 for v in prod.values()), priv
     moved = rm.default_scene()
     moved[0].center[0] = 14.0
     rc2, co2 = _code_object(rm, moved)
@@ -140,9 +141,10 @@ def test_table_specialises_without_a_device(rm):
 
 def test_table_compiles_once(rm, tmp_path):
     """rm_scene_specialize compiles the reference scene's table once.
-    The unbounded build's kernel descriptors give the production kernels' VGPR
-    allocation (72: 7 waves per SIMD, no scratch), so no occupancy ladder runs; the
-    hiprtc invocations are counted from RM_JIT_LOG's one line per compile."""
+    The 8-wave build's kernel descriptors show at most 32 B of scratch per lane for
+    the production kernels (64 VGPRs, 8 waves per SIMD), so no other bound is
+    compiled; the hiprtc invocations are counted from RM_JIT_LOG's one line per
+    compile."""
     import subprocess
     import sys
     prog = (
@@ -163,7 +165,7 @@ def test_table_compiles_once(rm, tmp_path):
     assert rc == 0
     vg = _kernel_vgprs(co)
     prod = {k: v for k, v in vg.items() if "ILb0E" in k}
-    assert len(prod) == 2 and all(v <= 72 for v in prod.values()), vg  # >= 7 waves per SIMD
+    assert len(prod) == 2 and all(v <= 64 for v in prod.values()), vg  # 8 waves per SIMD
 
 
 def _kernel_vgprs(co):
