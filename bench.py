@@ -152,8 +152,10 @@ def cpu_baseline(args, cfg, u, f):
     import tempfile
     import oracle as O  # test/baseline infrastructure only
     W, H = cfg["width"], cfg["height"]
+    # the whole frame for every BASELINE config (cfg5, the largest: ~7 s per build
+    # on the box's 16 CPUs); every 4th row only beyond that
     stride = args.cpu_row_stride or (1 if W * H * (4 if cfg["aa"] else 1) * max(cfg["bounces"], 1)
-                                     <= 3840 * 2160 * 4 * 3 else 4)
+                                     <= 7680 * 4320 * 4 * 5 else 4)
     rows = list(range(0, H, stride))
     sh = cpu_share()
     threads = args.cpu_threads or sh["share"]
@@ -325,7 +327,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=0,
                     help="cpu_baseline renders every k-th row of one frame (0: the whole "
-                         "frame for configs 1-3, every 4th row for the 8K / 5-bounce ones)")
+                         "frame for every BASELINE config)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = nproc, capped at the CPUs this process may run on")
     args = ap.parse_args()
