@@ -23,11 +23,12 @@ ORACLE   := oracle/_build/librm_oracle.so
 DRIVER   := $(PKG)/rm_frameloop
 
 RM_SRCS  := $(CSRC)/rm_api.hip $(CSRC)/rm_kernels.hip $(CSRC)/rm_table.hip $(CSRC)/rm_jit.hip $(CSRC)/rm_host.cpp $(CSRC)/rm_comm.cpp
-RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp $(CSRC)/rm_jit.hpp $(CSRC)/rm_comm.hpp include/rm_api.h Makefile
+RM_HDRS  := $(CSRC)/rm_scene.hpp $(CSRC)/rm_shard.hpp $(CSRC)/rm_fastmath.hpp $(CSRC)/rm_internal.hpp $(CSRC)/rm_jit.hpp $(CSRC)/rm_comm.hpp include/rm_api.h Makefile
 # The table kernel's sources, embedded in librm.so for hiprtc (rm_jit.hip), under
 # the names they #include each other by.
 JIT_SRCS := rm_table.hip=$(CSRC)/rm_table.hip rm_internal.hpp=$(CSRC)/rm_internal.hpp \
-            rm_scene.hpp=$(CSRC)/rm_scene.hpp rm_fastmath.hpp=$(CSRC)/rm_fastmath.hpp \
+            rm_scene.hpp=$(CSRC)/rm_scene.hpp rm_shard.hpp=$(CSRC)/rm_shard.hpp \
+            rm_fastmath.hpp=$(CSRC)/rm_fastmath.hpp \
             ../../include/rm_api.h=include/rm_api.h
 
 .PHONY: all librm oracle driver goldens clean

@@ -68,6 +68,14 @@ CONFIGS = {
 }
 SWEEP_FRAMES = 120
 
+# Rank 0 also assembles every gathered frame (k_unshard, HBM-bound: 2 x the RGBA8
+# image at ~6.4 TB/s).  Its time over one GPU's render time of the whole frame, per
+# config, measured on one MI355X (tools/probe_unshard.py, profiles/r05_unshard.txt;
+# frame times of DESIGN §9): --rank0-share -1 gives rank 0 the rows per round that
+# balance its render + assembly against the other ranks' render
+# (rm.best_rank0_rows).
+ASSEMBLE_RATIO = {1: 0.25, 2: 0.060, 3: 0.0126, 4: 0.0117, 5: 0.0135}
+
 
 def bench_frames(steps: int) -> list:
     """Sweep frames of the K timed steps: step k renders frame floor(k * 120 / K), so
@@ -244,6 +252,7 @@ def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
             vals[k].append(ph[k] / len(chunk))
     r.enable_timing(False)
     r.kernel_time_ms(reset=True)
+    vals["render_plus_assemble_ms"] = [a + b for a, b in zip(vals["render_ms"], vals["assemble_ms"])]
     mine = {"rank": rank}
     for k, v in vals.items():
         mine[k.replace("_ms", "_mean_ms")] = round(float(np.mean(v)), 4)
@@ -257,6 +266,10 @@ def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
             "max_gather_mean_ms": max(p["gather_mean_ms"] for p in allp),
             "max_gather_max_ms": max(p["gather_max_ms"] for p in allp),
             "assemble_mean_ms": allp[0]["assemble_mean_ms"],
+            # rank 0 renders its (smaller, --rank0-share) shard and assembles; the others
+            # render: balanced when rank 0's sum is at most the largest other render
+            "rank0_render_plus_assemble_mean_ms": allp[0]["render_plus_assemble_mean_ms"],
+            "max_other_render_mean_ms": max((p["render_mean_ms"] for p in allp[1:]), default=None),
             "note": "every timed frame re-rendered eagerly after the timed region, one "
                     + ("frame" if batch == 1 else f"batch of {batch} frames (values per frame)")
                     + " at a time; gather_ms runs from this rank's render end to its gather end, "
@@ -293,6 +306,11 @@ def main() -> int:
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--row-block", type=int, default=8,
                     help="rows per interleaved block when sharding over ranks")
+    ap.add_argument("--rank0-share", type=float, default=-1.0,
+                    help="N > 1: rank 0's rows per round as a share of --row-block (rank 0 also "
+                         "assembles every frame, so it renders fewer rows: rm_config.rank0_rows = "
+                         "round(share x row_block)); -1 = the share that balances rank 0's render + "
+                         "assembly against the other ranks' render for this config (ASSEMBLE_RATIO)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: replay the frame from a captured hipGraph (rm_graph_dispatch); "
                          "default: on for config 5 (BASELINE 'hipGraph-captured frame')")
@@ -385,7 +403,13 @@ def main() -> int:
             ucache[f] = rm.sweep_uniforms(f, SWEEP_FRAMES, cfg["bounces"], cfg["aa"], cfg["shadow"])
         return ucache[f]
 
-    shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws) if dist_on else {}
+    # the weighted interleave (rm_config.rank0_rows, rm_shard.hpp): rank 0's rows per round
+    if args.rank0_share > 0:
+        rank0_rows = max(1, int(round(args.rank0_share * args.row_block)))
+    else:
+        rank0_rows = rm.best_rank0_rows(args.row_block, ws, ASSEMBLE_RATIO[args.config]) if ws > 1 else 0
+    shard_args = (dict(row_block=args.row_block, shard=rank, nshards=ws, rank0_rows=rank0_rows)
+                  if dist_on else {})
     rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
           for _ in range(nfl)]
     if dist_on:
@@ -557,7 +581,7 @@ def main() -> int:
     cnt_total = None
     with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, counters=True, device=local,
                      row_block=args.row_block if dist_on else 0, shard=rank if dist_on else 0,
-                     nshards=ws) as rc:
+                     nshards=ws, rank0_rows=rank0_rows if dist_on else 0) as rc:
         if scene is not None:
             use_scene(rc)
         seen = {}
@@ -596,7 +620,7 @@ def main() -> int:
     # the frames timed): the kernel skips most of it by proof, so this rate is not
     # hardware utilisation and can exceed the peak.
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
-    bytes_per_launch = (rm.shard_rows_cap(H, args.row_block, ws) if dist_on else H) * W * 4
+    bytes_per_launch = (rm.shard_rows_cap(H, args.row_block, ws, rank0_rows) if dist_on else H) * W * 4
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
 
     # ---- CPU baseline + parity sample (rank 0, N = 1 only) ----
@@ -652,7 +676,10 @@ def main() -> int:
                        "communicators_per_rank": (1 if one_comm else nfl) if dist_on else 0,
                        "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
                                        + (" (pipelined)" if args.pipeline else "")
-                                       if dist_on else "single GPU")},
+                                       if dist_on else "single GPU"),
+                       "rank0_rows_per_round": (rank0_rows or args.row_block) if dist_on else None,
+                       "rows_per_rank": ([rm.shard_rows(H, args.row_block, ws, s_, rank0_rows)[0]
+                                          for s_ in range(ws)] if dist_on else None)},
             "fps": round(frames / elapsed, 3),
             # host time to issue the K steps (rank 0): well below ms_per_step = GPU-bound
             "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4),

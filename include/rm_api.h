@@ -36,8 +36,8 @@
 extern "C" {
 #endif
 
-#define RM_API_VERSION 4
-#define RM_CONFIG_MAGIC 0x34434D52u /* "RMC4" little-endian: rm_config layout of API version 4 */
+#define RM_API_VERSION 5
+#define RM_CONFIG_MAGIC 0x35434D52u /* "RMC5" little-endian: rm_config layout of API version 5 */
 
 /* ---- status codes --------------------------------------------------------- */
 #define RM_OK 0
@@ -123,13 +123,19 @@ typedef struct rm_config {
   int32_t kernel;     /* RM_KERNEL_*; 0 = auto */
   int32_t counters;   /* nonzero: collect rm_counters + per-pixel sdf counts (slower) */
   /* Row sharding (multi-GPU): the image's rows are cut into
-   * blocks of row_block rows; block b belongs to shard b % nshards.  This
-   * context renders only shard `shard`'s rows, packed in block order, into a
-   * [rows_cap][width] image (rows_cap = rm_shard_rows_cap()).  nshards <= 1
-   * means the whole image. */
+   * rounds; a round holds rank0_rows rows of shard 0, then row_block rows of
+   * shard 1, 2, ..., nshards-1 (rank0_rows = row_block: block b belongs to
+   * shard b % nshards).  This context renders only shard `shard`'s rows, packed
+   * in round order, into a [rows_cap][width] image (rows_cap = rm_shard_rows()).
+   * nshards <= 1 means the whole image. */
   int32_t row_block;
   int32_t shard;
   int32_t nshards;
+  /* Rows of shard 0 per round (API version 5); 0 = row_block.  Shard 0 is the
+   * rank that assembles every gathered frame (k_unshard), so fewer rows for it
+   * balance its render + assembly against the other ranks' render
+   * (rm_shard_rows; bench.py --rank0-share). */
+  int32_t rank0_rows;
   /* Multi-GPU frames in one process.  ngpus >= 1 makes the
    * context drive ngpus devices: devices[0..ngpus), or device, device+1, ...
    * when devices is NULL (device -1 = the current device).  Device i renders
@@ -310,7 +316,7 @@ int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
 /* Assemble a full image from nshards packed shard images laid out
  * back-to-back ([nshards][rows_cap][width] RGBA8, e.g. the result of an RCCL
  * gather) into `frame` ([height][width] RGBA8), both device pointers, on the
- * context's stream. Uses the context's width/height/row_block/nshards. */
+ * context's stream. Uses the context's width/height/row_block/rank0_rows/nshards. */
 int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
 /* The same for frame k of an n-frame batch gathered as rm_dispatch_frames
  * gathers it: [nshards][n][rows_cap][width] RGBA8 (each rank's n shards back to
@@ -375,8 +381,25 @@ int rm_comm_rccl_info(rm_ctx *ctx, int32_t *count, int32_t *user_rank, int32_t *
                       int32_t *version);
 
 /* ---- row sharding helpers (pure functions) ------------------------------- */
-int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);
+/* The weighted interleave (API version 5).  Rows go in rounds of
+ * P = rank0_rows + (nshards - 1) row_block rows: shard 0 owns rows
+ * [kP, kP + rank0_rows) of round k, shard s >= 1 the row_block rows after
+ * rank0_rows + (s - 1) row_block.  Shard s's rows are packed in round order into
+ * a [rows_cap][width] image; rows_cap (the same for every shard, so one
+ * ncclGather moves them) is the largest shard's rounds times its rows per round,
+ * and *rows is shard s's own count of real rows.  rank0_rows = 0 means
+ * row_block (the plain interleave: block b belongs to shard b % nshards).
+ * nshards <= 1: the whole image (rows = rows_cap = height). */
+int rm_shard_rows(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t shard,
+                  int32_t *rows, int32_t *rows_cap);
 /* Global row (py) of local row `local_row` of shard `shard`; -1 if padding. */
+int32_t rm_shard_row(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t shard, int32_t nshards,
+                     int32_t local_row);
+/* The inverse: the shard and local row that own global row `row`. */
+int rm_shard_owner(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t row,
+                   int32_t *shard, int32_t *local_row);
+/* The plain interleave (rank0_rows = row_block), API version 1. */
+int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);
 int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
                             int32_t local_row);
 

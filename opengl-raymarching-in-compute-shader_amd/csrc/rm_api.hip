@@ -26,7 +26,7 @@ hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy);
 bool table_slazy(const uint32_t* words, int32_t n);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
+                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
 hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
 }  // namespace rm
 static_assert(RM_MAX_BATCH == rmd::kMaxBatch, "rm_api.h RM_MAX_BATCH == rm_scene.hpp kMaxBatch");
@@ -172,6 +172,8 @@ int image_rows(const rm_ctx* c) {
   return c->rows;
 }
 bool full_frame(const rm_ctx* c) { return c->cfg.nshards <= 1 || !c->subs.empty() || comm_root(c); }
+// Shard 0's rows per round (rm_config.rank0_rows; 0 = row_block, rm_shard.hpp).
+int row_block0(const rm_ctx* c) { return c->cfg.rank0_rows > 0 ? c->cfg.rank0_rows : c->cfg.row_block; }
 
 int nccl_fail(rm_ctx* c, const rm::Rccl* r, ncclResult_t e, const char* what) {
   return fail(c, RM_ERR_COMM, std::string(what) + ": " + (r ? r->GetErrorString(e) : "RCCL"));
@@ -538,6 +540,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.width = c->cfg.width;
   F.height = c->cfg.height;
   F.row_block = c->cfg.row_block;
+  F.row_block0 = row_block0(c);
   F.shard = c->cfg.shard;
   F.nshards = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
   F.rows = c->rows;
@@ -826,12 +829,12 @@ int comm_assemble(rm_ctx* c) {
   if (!comm_root(c)) return RM_OK;
   if (c->cfg.outputs & RM_OUT_RGBA8) {
     const hipError_t e = rm::launch_unshard(c->d_gathered, image_rgba8(c), c->cfg.width, c->cfg.height,
-                                            c->cfg.row_block, c->cranks, c->rows, c->stream);
+                                            c->cfg.row_block, row_block0(c), c->cranks, c->rows, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   }
   if (c->cfg.outputs & RM_OUT_RGBA32F) {
     const hipError_t e = rm::launch_unshard(c->d_gathered32, c->d_frame32, c->cfg.width * 4, c->cfg.height,
-                                            c->cfg.row_block, c->cranks, c->rows, c->stream);
+                                            c->cfg.row_block, row_block0(c), c->cranks, c->rows, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "unshard launch (RGBA32F)");
   }
   return RM_OK;
@@ -904,9 +907,10 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown output bits");
   if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_PIXEL)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
-  if (cfg->nshards > 1 &&
-      (cfg->row_block <= 0 || cfg->shard < 0 || cfg->shard >= cfg->nshards))
-    return fail(nullptr, RM_ERR_INVALID, "rm_create: bad row_block/shard/nshards");
+  if (cfg->nshards > 1 && rm_shard_rows(cfg->height, cfg->row_block, cfg->rank0_rows, cfg->nshards, cfg->shard,
+                                         nullptr, nullptr) != RM_OK)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: bad row_block/rank0_rows/shard/nshards (rm_shard_rows)");
+  if (cfg->rank0_rows < 0) return fail(nullptr, RM_ERR_INVALID, "rm_create: rank0_rows must be >= 0");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(nullptr, RM_ERR_NO_DEVICE,
@@ -938,7 +942,8 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     return code;
   };
   if ((rc = set_device(c)) != RM_OK) return bail(rc);
-  rm_shard_rows_cap(c->cfg.height, c->cfg.row_block, c->cfg.nshards, &c->rows);
+  rm_shard_rows(c->cfg.height, c->cfg.row_block, c->cfg.rank0_rows, c->cfg.nshards, c->cfg.shard, nullptr,
+                &c->rows);
   const size_t npx = (size_t)c->rows * (size_t)c->cfg.width;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return bail(hip_fail(c, e, "hipStreamCreate"));
@@ -1368,19 +1373,19 @@ int batch_finish(rm_ctx* c, int n) {
   const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
   if ((rc = phase(c, 2, c->gstream)) != RM_OK) return rc;
   if (comm_root(c)) {
-    const int W = c->cfg.width, H = c->cfg.height, rb = c->cfg.row_block;
+    const int W = c->cfg.width, H = c->cfg.height, rb = c->cfg.row_block, rb0 = row_block0(c);
     const size_t stride = (size_t)n * (size_t)c->rows;  // rows between two ranks' blocks
     for (int k = 0; k < n; ++k) {
       if (b.send8) {
         void* dst = k < n - 1 ? (void*)c->ring8[k] : (void*)image_rgba8(c);
-        const hipError_t e = rm::launch_unshard(b.send8 + (size_t)k * px * 4, dst, W, H, rb, c->cranks, c->rows,
-                                                c->gstream, stride);
+        const hipError_t e = rm::launch_unshard(b.send8 + (size_t)k * px * 4, dst, W, H, rb, rb0, c->cranks,
+                                                c->rows, c->gstream, stride);
         if (e != hipSuccess) return hip_fail(c, e, "unshard launch (batch)");
       }
       if (b.send32) {
         void* dst = k < n - 1 ? (void*)c->ring32[k] : (void*)c->d_frame32;
-        const hipError_t e = rm::launch_unshard(b.send32 + (size_t)k * px * 4, dst, W * 4, H, rb, c->cranks,
-                                                c->rows, c->gstream, stride);
+        const hipError_t e = rm::launch_unshard(b.send32 + (size_t)k * px * 4, dst, W * 4, H, rb, rb0,
+                                                c->cranks, c->rows, c->gstream, stride);
         if (e != hipSuccess) return hip_fail(c, e, "unshard launch (batch, RGBA32F)");
       }
     }
@@ -1845,7 +1850,7 @@ int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   hipError_t e = rm::launch_unshard(gathered_dev, frame_dev, c->cfg.width, c->cfg.height,
-                                    c->cfg.row_block, c->cfg.nshards, c->rows, c->stream);
+                                    c->cfg.row_block, row_block0(c), c->cfg.nshards, c->rows, c->stream);
   if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }
@@ -1859,7 +1864,7 @@ int rm_unshard_batch_rgba8(rm_ctx* c, const void* gathered_dev, int32_t k, int32
   const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
   const uint8_t* src = static_cast<const uint8_t*>(gathered_dev) + (size_t)k * px * 4;
   hipError_t e = rm::launch_unshard(src, frame_dev, c->cfg.width, c->cfg.height, c->cfg.row_block,
-                                    c->cfg.nshards, c->rows, c->stream, (size_t)n * (size_t)c->rows);
+                                    row_block0(c), c->cfg.nshards, c->rows, c->stream, (size_t)n * (size_t)c->rows);
   if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }

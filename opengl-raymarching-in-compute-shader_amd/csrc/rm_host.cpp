@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "rm_internal.hpp"
+#include "rm_shard.hpp"
 
 namespace {
 
@@ -347,29 +348,66 @@ int rm_sweep_uniforms(int32_t frame, int32_t nframes, int32_t bounceVar, int32_t
   return RM_OK;
 }
 
-// ---- row sharding: interleaved blocks of row_block rows -------
-int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t* rows_cap) {
-  if (!rows_cap || height <= 0) return RM_ERR_INVALID;
+// ---- row sharding: the weighted interleave of rm_shard.hpp ------
+// A valid map for (row_block, rank0_rows, nshards >= 2): rows per round fit in
+// 2^30 (so every row index below stays in int32).
+static bool shard_map(int32_t row_block, int32_t rank0_rows, int32_t nshards, rm::ShardMap* m) {
+  if (row_block <= 0 || rank0_rows < 0 || nshards < 2) return false;
+  m->rb = row_block;
+  m->rb0 = rank0_rows ? rank0_rows : row_block;
+  m->n = nshards;
+  return (int64_t)m->rb0 + (int64_t)(nshards - 1) * row_block <= (int64_t)1 << 30;
+}
+
+int rm_shard_rows(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t shard,
+                  int32_t* rows, int32_t* rows_cap) {
+  if (height <= 0 || height > 65536) return RM_ERR_INVALID;
   if (nshards <= 1) {
-    *rows_cap = height;
+    if (shard != 0) return RM_ERR_INVALID;
+    if (rows) *rows = height;
+    if (rows_cap) *rows_cap = height;
     return RM_OK;
   }
-  if (row_block <= 0) return RM_ERR_INVALID;
-  int32_t nblocks = (height + row_block - 1) / row_block;
-  int32_t per = (nblocks + nshards - 1) / nshards;
-  *rows_cap = per * row_block;
+  rm::ShardMap m;
+  if (!shard_map(row_block, rank0_rows, nshards, &m) || shard < 0 || shard >= nshards) return RM_ERR_INVALID;
+  if (rows) *rows = rm::shard_real_rows(m, height, shard);
+  if (rows_cap) *rows_cap = rm::shard_rows_cap(m, height);
   return RM_OK;
+}
+
+int32_t rm_shard_row(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t shard, int32_t nshards,
+                     int32_t local_row) {
+  if (local_row < 0 || height <= 0 || height > 65536) return -1;
+  if (nshards <= 1) return (shard == 0 && local_row < height) ? local_row : -1;
+  rm::ShardMap m;
+  if (!shard_map(row_block, rank0_rows, nshards, &m) || shard < 0 || shard >= nshards) return -1;
+  if (local_row >= rm::shard_rows_cap(m, height)) return -1;
+  const int32_t g = rm::shard_row(m, shard, local_row);
+  return g < height ? g : -1;
+}
+
+int rm_shard_owner(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t row,
+                   int32_t* shard, int32_t* local_row) {
+  if (!shard || !local_row || height <= 0 || height > 65536 || row < 0 || row >= height) return RM_ERR_INVALID;
+  if (nshards <= 1) {
+    *shard = 0;
+    *local_row = row;
+    return RM_OK;
+  }
+  rm::ShardMap m;
+  if (!shard_map(row_block, rank0_rows, nshards, &m)) return RM_ERR_INVALID;
+  rm::shard_owner(m, row, shard, local_row);
+  return RM_OK;
+}
+
+int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t* rows_cap) {
+  if (!rows_cap) return RM_ERR_INVALID;
+  return rm_shard_rows(height, row_block, row_block, nshards, 0, nullptr, rows_cap);
 }
 
 int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
                             int32_t local_row) {
-  if (local_row < 0 || height <= 0) return -1;
-  if (nshards <= 1) return local_row < height ? local_row : -1;
-  if (row_block <= 0 || shard < 0 || shard >= nshards) return -1;
-  int32_t lb = local_row / row_block;
-  int32_t gb = lb * nshards + shard;
-  int32_t g = gb * row_block + local_row % row_block;
-  return g < height ? g : -1;
+  return rm_shard_row(height, row_block, row_block, shard, nshards, local_row);
 }
 
 }  // extern "C"

@@ -571,19 +571,18 @@ __global__ __launch_bounds__(64, 8) void k_sample_frames(FrameBatch B) {
 // r * rank_stride of `gathered` (rank_stride = rows_cap for [nshards][rows_cap]
 // [width]; n * rows_cap for one frame of a batch gathered as [nshards][n]
 // [rows_cap][width]).  One grid row per frame row: the source row (shard, local
-// row) is computed once per workgroup in scalar registers; lanes copy 16 B (4
-// pixels) each when rows are 16-B aligned (width % 4 == 0 and both images 16-B
-// aligned), one pixel otherwise.
+// row; rm_shard.hpp's weighted interleave) is computed once per workgroup in
+// scalar registers; lanes copy 16 B (4 pixels) each when rows are 16-B aligned
+// (width % 4 == 0 and both images 16-B aligned), one pixel otherwise.
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
-                                                 int height, int row_block, int nshards,
+                                                 int height, rm::ShardMap map,
                                                  size_t rank_stride) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   for (int y = blockIdx.y; y < height; y += gridDim.y) {  // gridDim.y <= 65535
-    const int b = y / row_block;
-    const int r = b % nshards;
-    const int lrow = (b / nshards) * row_block + y % row_block;
+    int r, lrow;
+    rm::shard_owner(map, y, &r, &lrow);
     const uint32_t* src = gathered + ((size_t)r * rank_stride + lrow) * (size_t)width;
     uint32_t* dst = frame + (size_t)y * (size_t)width;
     if (VEC) {
@@ -672,7 +671,9 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 
 #ifndef RM_KERNELS_AA_ONLY
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows) {
+                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows) {
+  if (nshards < 1 || row_block < 1 || row_block0 < 1) return hipErrorInvalidValue;
+  const rm::ShardMap map{row_block, row_block0, nshards};
   const size_t stride = rank_stride_rows ? rank_stride_rows : (size_t)rows_cap;
   // 16-B copies need 16-B rows (width % 4 == 0) and 16-B aligned images: the
   // C-ABI takes caller pointers, which may be offset
@@ -683,11 +684,9 @@ hipError_t launch_unshard(const void* gathered, void* frame, int width, int heig
   const uint32_t* g = static_cast<const uint32_t*>(gathered);
   uint32_t* f = static_cast<uint32_t*>(frame);
   if (vec)
-    hipLaunchKernelGGL(rmd::k_unshard<true>, grid, dim3(256), 0, s, g, f, width, height, row_block,
-                       nshards, stride);
+    hipLaunchKernelGGL(rmd::k_unshard<true>, grid, dim3(256), 0, s, g, f, width, height, map, stride);
   else
-    hipLaunchKernelGGL(rmd::k_unshard<false>, grid, dim3(256), 0, s, g, f, width, height, row_block,
-                       nshards, stride);
+    hipLaunchKernelGGL(rmd::k_unshard<false>, grid, dim3(256), 0, s, g, f, width, height, map, stride);
   return hipGetLastError();
 }
 #endif

@@ -19,6 +19,7 @@
 #endif
 
 #include "rm_fastmath.hpp"
+#include "rm_shard.hpp"
 
 namespace rmd {
 
@@ -97,6 +98,7 @@ struct Frame {
   int32_t aa;      // AA
   int32_t width, height;
   int32_t row_block, shard, nshards;
+  int32_t row_block0;    // shard 0's rows per round (rm_shard.hpp; = row_block unsharded)
   int32_t rows;          // rows this launch renders (height, or the shard's rows_cap)
   uint8_t* rgba8;        // [rows][width][4] or null
   float* rgba32f;        // [rows][width][4] or null
@@ -889,11 +891,10 @@ __device__ __forceinline__ int tile_col(int b, int gx, int G) {
   return (w0 + win > gx) ? b : w0 + (r & 7) * G + (r >> 3);  // ragged last window: natural order
 }
 
-// Global row of a launch-local row (row sharding).
+// Global row of a launch-local row (row sharding; rm_shard.hpp).
 __device__ __forceinline__ int global_row(const Frame& F, int local_row) {
   if (F.nshards <= 1) return local_row;
-  int lb = local_row / F.row_block;
-  int g = (lb * F.nshards + F.shard) * F.row_block + local_row % F.row_block;
+  const int g = rm::shard_row(rm::ShardMap{F.row_block, F.row_block0, F.nshards}, F.shard, local_row);
   return g < F.height ? g : -1;
 }
 

@@ -32,8 +32,8 @@ RM_ERR_NO_DEVICE = -4
 RM_ERR_STATE = -5
 RM_ERR_COMM = -6
 
-RM_API_VERSION = 4
-RM_CONFIG_MAGIC = 0x34434D52
+RM_API_VERSION = 5
+RM_CONFIG_MAGIC = 0x35434D52
 
 RM_MAX_BATCH = 32
 RM_OUT_RGBA8 = 1
@@ -82,7 +82,7 @@ class rm_config(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("magic", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
                 ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
                 ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32),
-                ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
+                ("rank0_rows", C.c_int32), ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
 class rm_camera_state(C.Structure):
@@ -183,6 +183,11 @@ _SIGS = {
     "rm_kernel_time_ms": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]),
     "rm_frame_phases": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double)]),
+    "rm_shard_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rm_shard_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rm_shard_owner": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rm_shard_rows_cap": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "rm_shard_global_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rm_camera_init": (C.c_int, [C.POINTER(rm_camera_state), C.c_int32, C.c_int32, C.c_float,
@@ -391,16 +396,17 @@ class Renderer:
     def __init__(self, width: int, height: int, *, outputs: int = RM_OUT_RGBA8,
                  kernel: int = RM_KERNEL_AUTO, counters: bool = False, device: int = -1,
                  row_block: int = 0, shard: int = 0, nshards: int = 1, ngpus: int = 0,
-                 devices: Optional[Sequence[int]] = None):
+                 devices: Optional[Sequence[int]] = None, rank0_rows: int = 0):
         """ngpus >= 1: one context over ngpus devices (`devices`, or device,
-        device+1, ...), shards gathered with RCCL on the first (rm_config.ngpus)."""
+        device+1, ...), shards gathered with RCCL on the first (rm_config.ngpus).
+        rank0_rows: shard 0's rows per round of the weighted interleave (0 = row_block)."""
         devs = (C.c_int32 * len(devices))(*devices) if devices else None
         if devices:
             ngpus = len(devices)
         cfg = rm_config(struct_size=C.sizeof(rm_config), magic=RM_CONFIG_MAGIC, width=width, height=height,
                         device=device, outputs=outputs, kernel=kernel,
                         counters=1 if counters else 0, row_block=row_block, shard=shard,
-                        nshards=nshards, ngpus=ngpus,
+                        nshards=nshards, rank0_rows=rank0_rows, ngpus=ngpus,
                         devices=C.cast(devs, C.POINTER(C.c_int32)) if devs else None)
         h = C.c_void_p()
         _check(lib().rm_create(C.byref(h), C.byref(cfg)))
@@ -408,9 +414,10 @@ class Renderer:
         self.width, self.height = width, height
         self.outputs = outputs if outputs else RM_OUT_RGBA8
         self.nshards, self.shard, self.row_block = max(nshards, 1), shard, row_block
+        self.rank0_rows = rank0_rows
         self.ngpus = ngpus
-        self.rows = (shard_rows_cap(height, row_block, nshards) if nshards > 1 and not ngpus
-                     else height)
+        self.rows = (shard_rows(height, row_block, nshards, shard, rank0_rows)[1]
+                     if nshards > 1 and not ngpus else height)
 
     # -- lifetime
     def close(self) -> None:
@@ -655,16 +662,48 @@ def glMemoryBarrier(p: Renderer) -> None:  # main.cpp:125
 
 
 # ---- row sharding ---------------------------------------------------------
-def shard_rows_cap(height: int, row_block: int, nshards: int) -> int:
-    v = C.c_int32(0)
-    _check(lib().rm_shard_rows_cap(height, row_block, nshards, C.byref(v)))
-    return v.value
+def shard_rows(height: int, row_block: int, nshards: int, shard: int = 0,
+               rank0_rows: int = 0) -> tuple:
+    """(real rows of `shard`, rows_cap) of the weighted interleave (rm_shard_rows)."""
+    n, cap = C.c_int32(0), C.c_int32(0)
+    _check(lib().rm_shard_rows(height, row_block, rank0_rows, nshards, shard, C.byref(n),
+                               C.byref(cap)))
+    return n.value, cap.value
 
 
-def shard_global_rows(height: int, row_block: int, shard: int, nshards: int) -> np.ndarray:
-    cap = shard_rows_cap(height, row_block, nshards)
-    return np.array([lib().rm_shard_global_row(height, row_block, shard, nshards, r)
+def shard_rows_cap(height: int, row_block: int, nshards: int, rank0_rows: int = 0) -> int:
+    return shard_rows(height, row_block, nshards, 0, rank0_rows)[1]
+
+
+def shard_global_rows(height: int, row_block: int, shard: int, nshards: int,
+                      rank0_rows: int = 0) -> np.ndarray:
+    """Global row of every local row of `shard` (-1: padding), rm_shard_row."""
+    cap = shard_rows_cap(height, row_block, nshards, rank0_rows)
+    return np.array([lib().rm_shard_row(height, row_block, rank0_rows, shard, nshards, r)
                      for r in range(cap)], np.int32)
+
+
+def shard_owner(height: int, row_block: int, nshards: int, row: int, rank0_rows: int = 0) -> tuple:
+    """(shard, local row) holding global row `row` (rm_shard_owner)."""
+    s, l = C.c_int32(0), C.c_int32(0)
+    _check(lib().rm_shard_owner(height, row_block, rank0_rows, nshards, row, C.byref(s), C.byref(l)))
+    return s.value, l.value
+
+
+def best_rank0_rows(row_block: int, nshards: int, assemble_ratio: float) -> int:
+    """Shard 0's rows per round that balance its render + the frame's assembly against
+    the other shards' render: the r0 in 1..2 row_block minimising
+    max(r0 / P + a, row_block / P), P = r0 + (nshards - 1) row_block, with a = the
+    assembly's time over one GPU's render time of the whole frame."""
+    if nshards <= 1:
+        return 0
+    best, arg = None, row_block
+    for r0 in range(1, 2 * row_block + 1):
+        P = r0 + (nshards - 1) * row_block
+        t = max(r0 / P + assemble_ratio, row_block / P)
+        if best is None or t < best - 1e-12:
+            best, arg = t, r0
+    return arg
 
 
 def quantize_rgba8(img: np.ndarray) -> np.ndarray:

@@ -44,7 +44,7 @@ def test_structs_match_header_sizes(rm):
     assert C.sizeof(rm.rm_light) == 60
     assert C.sizeof(rm.rm_uniforms) == 64 + 60 + 4 * 5 + 12 + 8 + 4
     assert C.sizeof(rm.rm_counters) == 56
-    assert C.sizeof(rm.rm_config) == 56  # struct_size + magic + 10 int32 + the devices pointer
+    assert C.sizeof(rm.rm_config) == 64  # struct_size + magic + 11 int32 + pad + the devices pointer
     assert C.sizeof(rm.rm_camera_state) == 8 + 24 + 48
 
 
@@ -74,7 +74,7 @@ def test_struct_layouts_match_the_c_compiler(rm, tmp_path):
 
 
 def test_api_version(rm):
-    assert rm.lib().rm_api_version() == 4 == rm.RM_API_VERSION
+    assert rm.lib().rm_api_version() == 5 == rm.RM_API_VERSION
 
 
 def test_config_struct_size_is_checked(rm):
@@ -90,10 +90,17 @@ def test_config_struct_size_is_checked(rm):
     assert rm.lib().rm_create(C.byref(h), C.byref(old)) == rm.RM_ERR_INVALID
     assert b"struct_size" in rm.lib().rm_last_error(None)
     assert not h.value
-    # a v3 host's struct has the same size (56 on LP64) and its second
-    # word is the width: the magic refuses it
+    # a v3 host's struct has the same size as v4's (56 on LP64) and its
+    # second word is the width: the magic refuses it
     v3 = rm.rm_config(struct_size=C.sizeof(rm.rm_config), magic=1920, width=1080)
     assert rm.lib().rm_create(C.byref(h), C.byref(v3)) == rm.RM_ERR_INVALID
+    assert b"magic" in rm.lib().rm_last_error(None)
+    assert not h.value
+    # a v4 host (magic "RMC4", 56 bytes, no rank0_rows) is refused by size and magic
+    v4 = rm.rm_config(struct_size=56, magic=0x34434D52, width=64, height=32)
+    assert rm.lib().rm_create(C.byref(h), C.byref(v4)) == rm.RM_ERR_INVALID
+    v4.struct_size = C.sizeof(rm.rm_config)
+    assert rm.lib().rm_create(C.byref(h), C.byref(v4)) == rm.RM_ERR_INVALID
     assert b"magic" in rm.lib().rm_last_error(None)
     assert not h.value
 
@@ -128,6 +135,9 @@ def test_argument_validation_without_gpu(rm):
     assert e.value.code == rm.RM_ERR_INVALID
     with pytest.raises(rm.RMError):
         rm.Renderer(16, 16, nshards=2, row_block=0)
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(16, 16, nshards=2, row_block=8, rank0_rows=-1)
+    assert e.value.code == rm.RM_ERR_INVALID
     with pytest.raises(rm.RMError):
         rm.sweep_uniforms(0, 120, bounces=6)
 

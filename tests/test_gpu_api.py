@@ -136,18 +136,22 @@ def test_kernel_timing(rm, gpu):
 
 
 @pytest.mark.parametrize("aa", [True, False], ids=["k_sample", "k_pixel"])
-@pytest.mark.parametrize("N,R", [(2, 8), (3, 4), (8, 8)])
+@pytest.mark.parametrize("N,R,R0", [(2, 8, 8), (3, 4, 4), (8, 8, 8), (2, 8, 7), (4, 8, 5), (8, 8, 7),
+                                    (3, 4, 9)])
 @pytest.mark.parametrize("W", [80, 83])  # 16-B row copies / per-pixel copies in k_unshard
-def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, W):
+def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, R0, W):
+    """Virtual ranks of the (weighted) interleave: every shard
+    rendered into its slot of one gather buffer and assembled by k_unshard equals
+    the full render byte for byte."""
     import torch
     H = 61
     k = rm.RM_KERNEL_PIXEL
     u = rm.sweep_uniforms(70, 120, 3, aa, 0)
     full = render(rm, u, W, H, kernel=k)
-    cap = rm.shard_rows_cap(H, R, N)
+    cap = rm.shard_rows_cap(H, R, N, R0)
     gathered = torch.zeros((N, cap, W, 4), dtype=torch.uint8, device="cuda")
     frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-    rs = [rm.Renderer(W, H, kernel=k, row_block=R, shard=i, nshards=N) for i in range(N)]
+    rs = [rm.Renderer(W, H, kernel=k, row_block=R, shard=i, nshards=N, rank0_rows=R0) for i in range(N)]
     for i, r in enumerate(rs):
         r.set_output_rgba8(gathered[i].data_ptr())
         r.dispatch(u)

@@ -215,8 +215,8 @@ def test_batch_full_size(rm, gpu, cfg):
             np.testing.assert_array_equal(r.read_frame_rgba8(k), one.read_rgba8(), err_msg=f"frame {frames[k]}")
 
 
-@pytest.mark.parametrize("N,R,n", [(2, 8, 5), (3, 4, 3), (8, 8, 4)])
-def test_batch_gather_layout_assembles(rm, gpu, N, R, n):
+@pytest.mark.parametrize("N,R,R0,n", [(2, 8, 8, 5), (3, 4, 4, 3), (8, 8, 8, 4), (8, 8, 7, 4), (4, 8, 6, 3)])
+def test_batch_gather_layout_assembles(rm, gpu, N, R, R0, n):
     """The N-rank layout of a gathered batch, rehearsed with N virtual ranks on one GPU
     (RCCL refuses two ranks on one device): rank r's n shards rendered by
     rm_dispatch_frames, placed as ncclGather places them on rank 0 ([N][n][rows_cap]
@@ -226,15 +226,15 @@ def test_batch_gather_layout_assembles(rm, gpu, N, R, n):
     import torch
     W, H = 160, 90
     us = _frames(rm, n)
-    cap = rm.shard_rows_cap(H, R, N)
+    cap = rm.shard_rows_cap(H, R, N, R0)
     gathered = torch.zeros((N, n, cap, W, 4), dtype=torch.uint8, device="cuda")
     for r in range(N):
-        with rm.Renderer(W, H, row_block=R, shard=r, nshards=N) as s:
+        with rm.Renderer(W, H, row_block=R, shard=r, nshards=N, rank0_rows=R0) as s:
             s.dispatch_frames(us)
             for k in range(n):
                 gathered[r, k] = torch.from_numpy(s.read_frame_rgba8(k)).cuda()
     ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
-    with rm.Renderer(W, H, row_block=R, shard=0, nshards=N) as a:
+    with rm.Renderer(W, H, row_block=R, shard=0, nshards=N, rank0_rows=R0) as a:
         for k in range(n):
             frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
             torch.cuda.synchronize()

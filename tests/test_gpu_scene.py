@@ -167,23 +167,24 @@ def test_table_graph_replay(rm, gpu):
         np.testing.assert_array_equal(r.read_rgba32f(), ref["rgba32f"])
 
 
-def test_table_shards_assemble(rm, gpu):
+@pytest.mark.parametrize("R0", [4, 3])
+def test_table_shards_assemble(rm, gpu, R0):
     W, H, N, R = 64, 50, 3, 4
     sc = random_scene(rm, 3)
     u = rm.sweep_uniforms(40, 120, 2, True, 0)
     full = _render(rm, u, W, H, scene=sc, counters=False)["rgba8"]
     cap = C.c_int32(0)
-    rm.lib().rm_shard_rows_cap(H, R, N, C.byref(cap))
+    rm.lib().rm_shard_rows(H, R, R0, N, 0, None, C.byref(cap))
     parts = []
     for s in range(N):
-        with rm.Renderer(W, H, row_block=R, shard=s, nshards=N) as r:
+        with rm.Renderer(W, H, row_block=R, shard=s, nshards=N, rank0_rows=R0) as r:
             r.set_scene(sc)
             r.dispatch(u)
             parts.append(r.read_rgba8())
     got = np.zeros_like(full)
     for s in range(N):
         for lr in range(cap.value):
-            g = rm.lib().rm_shard_global_row(H, R, s, N, lr)
+            g = rm.lib().rm_shard_row(H, R, R0, s, N, lr)
             if g >= 0:
                 got[g] = parts[s][lr]
     np.testing.assert_array_equal(got, full)

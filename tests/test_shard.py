@@ -31,29 +31,124 @@ def test_rows_partition_exactly(rm, H, R, N):
 def test_single_shard_is_identity(rm):
     assert rm.shard_rows_cap(100, 8, 1) == 100
     assert list(rm.shard_global_rows(10, 8, 0, 1)) == list(range(10))
+    assert rm.shard_rows(100, 8, 1, 0, 3) == (100, 100)
 
 
-def unshard_np(gathered, H, R, N):
-    """numpy model of k_unshard (rm_kernels.hip)."""
+def _rounds_model(H, R, R0, N):
+    """Independent model of the weighted interleave (include/rm_api.h rm_shard_rows):
+    walk the rows round by round, handing R0 rows to shard 0 and R to each other."""
+    owner = []
+    while len(owner) < H:
+        for s in range(N):
+            owner.extend([s] * (R0 if s == 0 else R))
+    return owner[:H]
+
+
+WEIGHTED = [(H, R, R0, N) for N in range(1, 9) for H in (1, 7, 63, 64, 65, 541, 2160, 4319)
+            for R, R0 in ((8, 8), (8, 7), (8, 5), (8, 1), (4, 9), (1, 1), (3, 2))]
+
+
+@pytest.mark.parametrize("H,R,R0,N", WEIGHTED)
+def test_weighted_schedule_properties(rm, H, R, R0, N):
+    """the weighted schedule is a pure function whose shards
+    partition the frame exactly, in round order, rank 0 taking R0 rows per round;
+    every shard image has the common rows_cap; owner() inverts row()."""
+    own = _rounds_model(H, R, R0, N)
+    cap = rm.shard_rows_cap(H, R, N, R0)
+    seen = np.full(H, -1)
+    for s in range(N):
+        rows, cap_s = rm.shard_rows(H, R, N, s, R0)
+        assert cap_s == cap
+        g = rm.shard_global_rows(H, R, s, N, R0)
+        real = g[g >= 0]
+        assert len(real) == rows and (g[:rows] >= 0).all() and (g[rows:] == -1).all()
+        assert (np.diff(real) > 0).all(), "packed in round order"
+        assert [own[y] for y in real] == [s] * rows if N > 1 else True
+        seen[real] = s
+        for j, y in enumerate(real.tolist()):
+            assert rm.shard_owner(H, R, N, y, R0) == (s, j)
+    assert (seen >= 0).all(), "every row owned by exactly one shard"
+    if N > 1:
+        assert list(seen) == own
+        # the cap is the smallest that holds every shard's rounds
+        per_round = [R0] + [R] * (N - 1)
+        P = sum(per_round)
+        need = []
+        for s in range(N):
+            off = sum(per_round[:s])
+            rounds = H // P + (1 if H % P > off else 0)
+            need.append(rounds * per_round[s])
+        assert cap == max(need)
+
+
+def test_weighted_default_is_plain_interleave(rm):
+    """rank0_rows = 0 and rank0_rows = row_block are the API-version-1 interleave."""
+    for H, R, N in ((2160, 8, 8), (37, 4, 3), (1080, 1, 7)):
+        for s in range(N):
+            a = rm.shard_global_rows(H, R, s, N)
+            assert (a == rm.shard_global_rows(H, R, s, N, R)).all()
+            assert [rm.lib().rm_shard_global_row(H, R, s, N, r) for r in range(len(a))] == a.tolist()
+
+
+def test_weighted_rank0_share_at_4k(rm):
+    """cfg3 at N = 8 with rank0_rows 7 of 8: rank 0 renders 7/63 of the rows."""
+    H, R, N = 2160, 8, 8
+    rows0, cap = rm.shard_rows(H, R, N, 0, 7)
+    rows1, _ = rm.shard_rows(H, R, N, 1, 7)
+    # 2160 = 34 * 63 + 18: the last round gives shard 0 its 7, shard 1 its 8, shard 2 three
+    assert rows0 == 7 * 35 and rows1 == 8 * 35 and cap == 8 * 35
+    assert sum(rm.shard_rows(H, R, N, s, 7)[0] for s in range(N)) == H
+
+
+def test_best_rank0_rows(rm):
+    # no assembly cost: the plain interleave; a larger one moves rows off rank 0
+    assert rm.best_rank0_rows(8, 8, 0.0) == 8
+    assert rm.best_rank0_rows(8, 8, 0.0111) == 7
+    assert rm.best_rank0_rows(8, 2, 0.0111) == 8
+    assert rm.best_rank0_rows(8, 8, 0.05) < 7
+    assert rm.best_rank0_rows(8, 1, 0.05) == 0
+
+
+def test_weighted_schedule_rejects_bad_maps(rm):
+    import ctypes as C
+    n, cap = C.c_int32(0), C.c_int32(0)
+    L = rm.lib()
+    assert L.rm_shard_rows(64, 8, -1, 2, 0, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
+    assert L.rm_shard_rows(64, 0, 8, 2, 0, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
+    assert L.rm_shard_rows(64, 8, 8, 2, 2, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
+    assert L.rm_shard_rows(64, 1 << 29, 8, 4, 0, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
+    assert L.rm_shard_row(64, 8, 7, 3, 2, 0) == -1
+    assert L.rm_shard_owner(64, 8, 7, 2, 64, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
+
+
+def unshard_np(gathered, H, R, N, R0=None):
+    """numpy model of k_unshard (rm_kernels.hip) over the weighted interleave."""
+    R0 = R if R0 is None else R0
     _, cap, W, _ = gathered.shape
     out = np.zeros((H, W, 4), gathered.dtype)
+    P = R0 + (N - 1) * R
     for y in range(H):
-        b = y // R
-        out[y] = gathered[b % N, (b // N) * R + y % R]
+        k, j = divmod(y, P)
+        if j < R0:
+            s, l = 0, k * R0 + j
+        else:
+            s, l = 1 + (j - R0) // R, k * R + (j - R0) % R
+        out[y] = gathered[s, l]
     return out
 
 
-def test_unshard_model_roundtrip(rm):
-    H, W, R, N = 37, 5, 4, 3
+@pytest.mark.parametrize("H,R,R0,N", [(37, 4, 4, 3), (37, 4, 3, 3), (130, 8, 7, 8), (65, 8, 1, 2)])
+def test_unshard_model_roundtrip(rm, H, R, R0, N):
+    W = 5
     img = np.random.default_rng(0).integers(0, 255, (H, W, 4), dtype=np.uint8)
-    cap = rm.shard_rows_cap(H, R, N)
+    cap = rm.shard_rows_cap(H, R, N, R0)
     g = np.zeros((N, cap, W, 4), np.uint8)
     for r in range(N):
-        rows = rm.shard_global_rows(H, R, r, N)
+        rows = rm.shard_global_rows(H, R, r, N, R0)
         for j, y in enumerate(rows):
             if y >= 0:
                 g[r, j] = img[y]
-    np.testing.assert_array_equal(unshard_np(g, H, R, N), img)
+    np.testing.assert_array_equal(unshard_np(g, H, R, N, R0), img)
 
 
 def _free_port():
@@ -64,7 +159,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, R, q):
+def _worker(rank, world, port, W, H, R, R0, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "opengl-raymarching-in-compute-shader_amd"))
@@ -77,7 +172,7 @@ def _worker(rank, world, port, W, H, R, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     u = rm.sweep_uniforms(40, 120, 2, True, 0)
-    rows = rm.shard_global_rows(H, R, rank, world)
+    rows = rm.shard_global_rows(H, R, rank, world, R0)
     shard = np.zeros((len(rows), W, 4), np.uint8)
     real = rows[rows >= 0]
     shard[: len(real)] = O.render(u, W, H, rows=real.tolist(), nthreads=2)["rgba8"]
@@ -86,17 +181,20 @@ def _worker(rank, world, port, W, H, R, q):
     dist.gather(t, gather_list=glist, dst=0)
     if rank == 0:
         g = torch.stack(glist).numpy()
-        q.put(unshard_np(g, H, R, world))
+        q.put(unshard_np(g, H, R, world, R0))
     dist.destroy_process_group()
 
 
-def test_gloo_gather_assembles_full_frame(rm, oracle):
+@pytest.mark.parametrize("R0", [8, 5])
+def test_gloo_gather_assembles_full_frame(rm, oracle, R0):
+    """world size 2 over gloo: oracle-rendered shards of the (weighted) interleave,
+    gathered to rank 0 and assembled, equal the full frame."""
     import multiprocessing as mp
     W, H, R, world = 48, 40, 8, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, W, H, R, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, W, H, R, R0, q)) for r in range(world)]
     for p in ps:
         p.start()
     img = q.get(timeout=300)
@@ -225,3 +323,6 @@ def test_bench_n_gt_1_report_over_gloo(bad_count):
         assert abs(ph["max_render_mean_ms"] - 0.2) < 1e-9 and abs(ph["max_render_max_ms"] - 0.2) < 1e-9
         assert abs(ph["per_rank"][0]["render_mean_ms"] - 0.1) < 1e-9
         assert abs(ph["assemble_mean_ms"] - 0.01) < 1e-9 and abs(ph["max_gather_mean_ms"] - 0.02) < 1e-9
+        assert abs(ph["rank0_render_plus_assemble_mean_ms"] - 0.11) < 1e-9
+        assert abs(ph["max_other_render_mean_ms"] - 0.2) < 1e-9
+        assert abs(ph["per_rank"][1]["render_plus_assemble_mean_ms"] - 0.2) < 1e-9
