@@ -31,7 +31,7 @@ JIT_SRCS := rm_table.hip=$(CSRC)/rm_table.hip rm_internal.hpp=$(CSRC)/rm_interna
             rm_fastmath.hpp=$(CSRC)/rm_fastmath.hpp \
             ../../include/rm_api.h=include/rm_api.h
 
-.PHONY: all librm oracle driver goldens clean
+.PHONY: all librm oracle driver goldens asan clean
 all: librm oracle driver
 librm: $(LIBRM)
 oracle: $(ORACLE)
@@ -104,6 +104,48 @@ oracle/_ref/gen_input_goldens: oracle/gen_input_goldens.cpp
 oracle/_ref/gen_camera_goldens: oracle/gen_camera_goldens.cpp
 	@mkdir -p oracle/_ref
 	$(CXX) -std=c++11 -O2 -ffp-contract=off -I$(REF)/includes -o $@ $<
+
+# ---- host sanitizer build: CPU suite under ASan + UBSan ---------
+# librm's host code (the C-ABI, the table compiler and its bounds, the uniform
+# lookup, input replay, the shard map, the hiprtc driver) and the oracle, built
+# with AddressSanitizer + UndefinedBehaviorSanitizer, every report fatal.  The
+# sanitizers are on the host side only (-Xarch_host; the device code is the
+# production build's): this build is for the CPU container, where no kernel runs
+# anyway (GPU sanitizers are not available).  tests/test_sanitizers.py runs the
+# host-logic CPU tests against it (LD_PRELOAD of clang's ASan runtime, RM_LIBRM,
+# RM_ORACLE).
+LLVM     ?= /opt/rocm/lib/llvm
+ASAN_DIR := $(PKG)/build/asan
+ASANLIB  := $(ASAN_DIR)/librm.so
+ASANORC  := oracle/_build/librm_oracle_asan.so
+SANHOST  := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+            -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer
+SANFLAGS := -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer
+ASAN_OBJS := $(addprefix $(ASAN_DIR)/,rm_api.o rm_kernels.o rm_kernels_aa.o rm_table.o rm_jit.o rm_host.o rm_comm.o)
+asan: $(ASANLIB) $(ASANORC)
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.hip $(RM_HDRS) $(PKG)/build/rm_jit_src.inc
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -O1 -g $(SANHOST) -I$(PKG)/build -c $< -o $@
+$(ASAN_DIR)/rm_kernels.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -O1 -g $(SANHOST) -DRM_KERNELS_PIXEL_ONLY -c $< -o $@
+$(ASAN_DIR)/rm_kernels_aa.o: $(CSRC)/rm_kernels.hip $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -O1 -g $(SANHOST) -DRM_KERNELS_AA_ONLY -c $< -o $@
+$(ASAN_DIR)/rm_host.o: $(CSRC)/rm_host.cpp $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(LLVM)/bin/clang++ -std=c++17 -O1 -g -fPIC -ffp-contract=off $(SANFLAGS) -c $< -o $@
+$(ASAN_DIR)/rm_comm.o: $(CSRC)/rm_comm.cpp $(RM_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -O1 -g $(SANHOST) -x hip -c $< -o $@
+$(ASANLIB): $(ASAN_OBJS)
+	$(LLVM)/bin/clang++ -shared -fPIC $(SANFLAGS) -shared-libsan -o $@ $^ -L/opt/rocm/lib -lamdhip64 -lhiprtc -ldl \
+	  -Wl,-rpath,/opt/rocm/lib
+$(ASANORC): oracle/rm_oracle.c oracle/rm_oracle.h include/rm_api.h
+	@mkdir -p $(dir $@)
+	$(LLVM)/bin/clang -std=c11 -O1 -g -ffp-contract=off -fno-fast-math -fopenmp -fPIC -Wall $(SANFLAGS) \
+	  -shared -shared-libsan -o $@ oracle/rm_oracle.c -lm -L$(LLVM)/lib -Wl,-rpath,$(LLVM)/lib
 
 clean:
 	rm -rf $(PKG)/build $(LIBRM) $(DRIVER) oracle/_build oracle/_ref

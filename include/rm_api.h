@@ -198,7 +198,8 @@ int rm_dispatch(rm_ctx *ctx);
  * communicator context (rm_comm_init, rm_config.ngpus) every rank renders its
  * shards of the n frames in one launch, one ncclGather moves all n shards, and
  * rank 0 assembles the n frames; the gather runs on a second stream of the
- * context, so the next batch renders while this one gathers.  Frames with a
+ * context, so the next batch renders while this one gathers (a consumer on the
+ * caller's own stream orders itself after it with rm_wait_output).  Frames with a
  * different AA setting render in separate launches; a runtime scene table
  * renders one launch per frame.  Not available with cfg.counters. */
 #define RM_MAX_BATCH 32
@@ -313,6 +314,15 @@ int rm_set_stream(rm_ctx *ctx, void *hip_stream);
 int rm_set_output_rgba8(rm_ctx *ctx, void *device_ptr);
 /* Device pointer of the RGBA8 image the next dispatch writes. */
 int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
+/* Orders `hip_stream` (hipStream_t as void*; NULL = the null stream) after every
+ * write to the context's images queued so far: work the caller enqueues on it
+ * afterwards sees the last dispatch's frames (API version 5).  Needed on a
+ * communicator context (rm_comm_init, rm_config.ngpus): a batch's gather and
+ * rank 0's assembly run on the context's internal gather stream, so frame n-1
+ * in rm_get_output_rgba8 / rm_set_output_rgba8's buffer (and the batch's ring)
+ * is not ordered by rm_set_stream's stream alone.  rm_synchronize and the
+ * readbacks wait for it as well.  Asynchronous: records events, waits on none. */
+int rm_wait_output(rm_ctx *ctx, void *hip_stream);
 /* Assemble a full image from nshards packed shard images laid out
  * back-to-back ([nshards][rows_cap][width] RGBA8, e.g. the result of an RCCL
  * gather) into `frame` ([height][width] RGBA8), both device pointers, on the

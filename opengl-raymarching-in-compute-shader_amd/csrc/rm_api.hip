@@ -110,6 +110,7 @@ struct rm_ctx {
   int bnext = 0, blast = -1;        // the next slot; the slot of the last batch
   hipStream_t gstream = nullptr;    // gathers + assembly of batches
   hipEvent_t gdone = nullptr;       // the last batch's work on gstream
+  hipEvent_t out_ev = nullptr;      // rm_wait_output: the tail of the context's stream
   bool gdone_pending = false;       // plain dispatches order after it
   // a multi-GPU context (rm_config.ngpus): one shard context per device, subs[0] = rank 0
   std::vector<rm_ctx*> subs;
@@ -563,6 +564,11 @@ rmd::Frame make_frame(const rm_ctx* c) {
 // along a unit ray and five bounces add 1.3e5 more, so a camera within 10^15
 // of the origin keeps them there; a frame whose camera is farther out (or not
 // finite) renders with the generic kernel.
+//
+// The light position is not bounded here: shadow rays (rd = light.position - pos,
+// unnormalised, glsl:184, 235) march with the full-range form (TLazy::dist ->
+// prim_dist<false>, rm_table.hip), so however far the light is, no shadow point
+// reaches the short form (tests/test_gpu_scene.py far-light case).
 const rm::JitTable* frame_jit(const rm_ctx* c, const rmd::Frame& F) {
   if (!c->jit) return nullptr;
   for (int i = 0; i < 3; ++i)
@@ -623,6 +629,8 @@ void free_all(rm_ctx* c) {
   }
   if (c->gdone) (void)hipEventDestroy(c->gdone);
   c->gdone = nullptr;
+  if (c->out_ev) (void)hipEventDestroy(c->out_ev);
+  c->out_ev = nullptr;
   if (c->gstream) (void)hipStreamDestroy(c->gstream);
   c->gstream = nullptr;
   for (auto& p : c->ev_pool) {
@@ -1301,8 +1309,17 @@ int slot_alloc(rm_ctx* c, rm_ctx::BatchSlot& b, int n) {
   if (!b.rendered) RM_HIP(c, hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
   if (!b.freed) RM_HIP(c, hipEventCreateWithFlags(&b.freed, hipEventDisableTiming));
   if (b.cap >= n) return RM_OK;
-  if (b.pending) RM_HIP(c, hipEventSynchronize(b.freed));
-  RM_HIP(c, hipStreamSynchronize(c->stream));
+  // the slot's last gather (gstream) and this rank's renders (stream) must be done
+  // before its buffers go: on a communicator context that wait is the bounded poll
+  // of every other communicator wait (a stalled peer is RM_ERR_COMM at the deadline,
+  // ADVICE r04), not an unbounded event / stream synchronise
+  if (c->comm) {
+    const int rc = comm_wait(c);
+    if (rc != RM_OK) return rc;
+  } else {
+    if (b.pending) RM_HIP(c, hipEventSynchronize(b.freed));
+    RM_HIP(c, hipStreamSynchronize(c->stream));
+  }
   if (b.send8) (void)hipFree(b.send8);
   if (b.send32) (void)hipFree(b.send32);
   b.send8 = nullptr;
@@ -1424,7 +1441,12 @@ int comm_batch(rm_ctx* c, const rm_uniforms* u, int n) {
   const std::vector<rm_ctx*> ms = comm_members(c);
   int rc = RM_OK;
   for (rm_ctx* m : ms)
-    if ((rc = batch_render(m, u, n)) != RM_OK) return m == c ? rc : fail(c, rc, m->err);
+    if ((rc = batch_render(m, u, n)) != RM_OK) {
+      if (m == c) return rc;
+      // a member's communicator failed (its bounded slot wait): the frame's whole
+      // group is aborted, as for any other member failure
+      return rc == RM_ERR_COMM ? comm_abort(c, m->err) : fail(c, rc, m->err);
+    }
   ncclResult_t e = r->GroupStart();
   if (e != ncclSuccess) return comm_abort(c, std::string("ncclGroupStart: ") + r->GetErrorString(e));
   for (rm_ctx* m : ms) {
@@ -1474,11 +1496,15 @@ int rm_dispatch_frames(rm_ctx* c, const rm_uniforms* u, int32_t n) {
     if (rc != RM_OK) return rc;
   }
   if (c->cfg.counters) return fail(c, RM_ERR_STATE, "rm_dispatch_frames: not available with counters");
+  // launch_batch walks c->u (and every member's) through the frames; a failed
+  // batch leaves the uniforms of the last successful dispatch
+  const rm_uniforms before = c->u;
   int rc;
   if (has_comm(c) && !c->group_member) rc = comm_batch(c, u, n);
   else rc = plain_batch(c, u, n);
-  c->u = u[n - 1];
-  for (rm_ctx* s : c->subs) s->u = u[n - 1];
+  const rm_uniforms& now = rc == RM_OK ? u[n - 1] : before;
+  c->u = now;
+  for (rm_ctx* s : c->subs) s->u = now;
   return rc;
 }
 
@@ -1841,6 +1867,25 @@ int rm_set_output_rgba8(rm_ctx* c, void* device_ptr) {
 int rm_get_output_rgba8(rm_ctx* c, void** device_ptr) {
   if (!c || !device_ptr) return RM_ERR_INVALID;
   *device_ptr = image_rgba8(c);
+  return RM_OK;
+}
+
+// The images live on the context's device (a multi-GPU context's: device 0).
+// Everything that writes them is on its stream, or for a communicator batch on
+// its gather stream, which the stream itself waits for before any later write
+// (order_after_batch); so the caller's stream waits for an event at the tail of
+// each.
+int rm_wait_output(rm_ctx* c, void* hip_stream) {
+  if (!c) return RM_ERR_INVALID;
+  rm_ctx* t = c->subs.empty() ? c : c->subs[0];
+  if (t->comm_failed || c->comm_failed) return comm_dead(c);
+  int rc = set_device(t);
+  if (rc != RM_OK) return fail(c, rc, t->err);
+  hipStream_t dst = static_cast<hipStream_t>(hip_stream);
+  if (!t->out_ev) RM_HIP(c, hipEventCreateWithFlags(&t->out_ev, hipEventDisableTiming));
+  RM_HIP(c, hipEventRecord(t->out_ev, t->stream));
+  RM_HIP(c, hipStreamWaitEvent(dst, t->out_ev, 0));
+  if (t->gstream) RM_HIP(c, hipStreamWaitEvent(dst, t->gdone, 0));
   return RM_OK;
 }
 

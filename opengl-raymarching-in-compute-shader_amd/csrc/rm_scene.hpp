@@ -768,10 +768,20 @@ __device__ __forceinline__ float shadow_min(float res, float k, float h, float t
   return gmin(res, kh / t);
 }
 
+// GLSL int(float) (glsl:79): truncation; a value outside the int range, which
+// GLSL leaves undefined, saturates and NaN gives 0: the
+// v_cvt_i32_f32 conversion itself, written out so that no compiler may assume
+// the C++ cast's undefined range away.
+__device__ __forceinline__ int glsl_int(float x) {
+  int r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // checkers(p) glsl:77-80
 __device__ __forceinline__ float checkers(f3 p) {
-  int a = (int)(1000.0f + p.x) % 2;
-  int b = (int)(1000.0f + p.z) % 2;
+  int a = glsl_int(1000.0f + p.x) % 2;
+  int b = glsl_int(1000.0f + p.z) % 2;
   return (a != b) ? 1.0f : 0.2f;
 }
 

@@ -177,6 +177,7 @@ _SIGS = {
     "rm_set_stream": (C.c_int, [_P, _P]),
     "rm_set_output_rgba8": (C.c_int, [_P, _P]),
     "rm_get_output_rgba8": (C.c_int, [_P, C.POINTER(_P)]),
+    "rm_wait_output": (C.c_int, [_P, _P]),
     "rm_unshard_rgba8": (C.c_int, [_P, _P, _P]),
     "rm_unshard_batch_rgba8": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P]),
     "rm_enable_timing": (C.c_int, [_P, C.c_int]),
@@ -573,6 +574,11 @@ class Renderer:
         p = C.c_void_p()
         _check(lib().rm_get_output_rgba8(self._h, C.byref(p)), self._h)
         return p.value or 0
+
+    def wait_output(self, stream_ptr: Optional[int]) -> None:
+        """Order the caller's stream after every image write queued so far
+        (rm_wait_output; a communicator batch assembles on an internal stream)."""
+        _check(lib().rm_wait_output(self._h, stream_ptr), self._h)
 
     def unshard_rgba8(self, gathered_ptr: int, frame_ptr: int) -> None:
         _check(lib().rm_unshard_rgba8(self._h, gathered_ptr, frame_ptr), self._h)

@@ -16,7 +16,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_HERE)
-ORACLE_SO = os.path.join(_HERE, "_build", "librm_oracle.so")
+# RM_ORACLE selects another build of the same source (the sanitizer build, `make asan`)
+ORACLE_SO = os.environ.get("RM_ORACLE", os.path.join(_HERE, "_build", "librm_oracle.so"))
 
 sys.path.insert(0, os.path.join(_ROOT, "opengl-raymarching-in-compute-shader_amd"))
 from rmarch import rm_counters, rm_primitive, rm_uniforms  # noqa: E402  (shared POD structs)

@@ -113,10 +113,22 @@ static inline hit H(float d, v3 c, int id, float m) {
   return h;
 }
 
+/* GLSL int(float) (glsl:79): truncation toward zero.  GLSL leaves a value outside
+ * the int range undefined (and C makes the cast undefined behaviour); the
+ * built-in contract takes the gfx950 conversion, v_cvt_i32_f32:
+ * saturating, NaN -> 0.  (x86's cvttss2si would give INT_MIN for every such
+ * value, whose parity differs from INT_MAX's; found by the sanitizer build.) */
+static inline int glsl_int(float x) {
+  if (!(x == x)) return 0;
+  if (x >= 2147483648.0f) return 2147483647;
+  if (x < -2147483648.0f) return -2147483647 - 1;
+  return (int)x;
+}
+
 /* glsl:77-80  checkers(p) */
 static inline v3 checkers(v3 p) {
-  return ((int)(1000.0f + p.x) % 2 != (int)(1000.0f + p.z) % 2) ? V(1.0f, 1.0f, 1.0f)
-                                                                 : V(0.2f, 0.2f, 0.2f);
+  return (glsl_int(1000.0f + p.x) % 2 != glsl_int(1000.0f + p.z) % 2) ? V(1.0f, 1.0f, 1.0f)
+                                                                       : V(0.2f, 0.2f, 0.2f);
 }
 /* glsl:83 */
 static inline float sdSphere(v3 p, float r) { return length3(p) - r; }

@@ -156,6 +156,71 @@ def test_batch_on_communicator_contexts(rm, gpu, form):
         _check_batch(rm, r, us[:2], ref[:2])
 
 
+@pytest.mark.parametrize("form", ["comm_init", "ngpus"])
+def test_wait_output_orders_a_caller_stream(rm, gpu, form):
+    """on a communicator context a batch's frame n-1 is assembled into
+    the caller's output buffer on the context's gather stream.  rm_wait_output
+    orders the caller's stream after it: a copy enqueued there afterwards (no host
+    sync in between) reads the finished frame."""
+    import torch
+    W, H = 160, 90
+    us = _frames(rm, 6)
+    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
+    s = torch.cuda.Stream()
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    if form == "ngpus":
+        r = rm.Renderer(W, H, ngpus=1, row_block=8)
+    else:
+        r = rm.Renderer(W, H, row_block=8, shard=0, nshards=1)
+        r.set_stream(s.cuda_stream)
+        r.comm_init(rm.comm_unique_id(), 1, 0)
+    with r:
+        r.set_output_rgba8(out.data_ptr())
+        for rep in range(3):
+            r.dispatch_frames(us[2 * rep:2 * rep + 2] + us[:3])
+            r.wait_output(s.cuda_stream)
+            with torch.cuda.stream(s):
+                got = out.clone()
+            s.synchronize()
+            np.testing.assert_array_equal(got.cpu().numpy(), ref[2][0], err_msg=f"rep {rep}")
+        r.dispatch(us[5])
+        r.wait_output(s.cuda_stream)
+        with torch.cuda.stream(s):
+            got = out.clone()
+        s.synchronize()
+        np.testing.assert_array_equal(got.cpu().numpy(), ref[5][0])
+
+
+def test_stalled_batch_slot_wait_is_bounded(rm, gpu):
+    """a batch longer than its slot re-allocates the slot after its
+    last gather; on a communicator context that wait is the bounded poll, so a
+    stream that does not drain (a spin kernel standing in for a stalled peer) is
+    RM_ERR_COMM at the deadline, not a hang; the failed batch leaves the
+    uniforms of the last good dispatch."""
+    import time
+    import torch
+    W, H = 64, 48
+    us = _frames(rm, 8)
+    s = torch.cuda.Stream()
+    r = rm.Renderer(W, H, row_block=8, shard=0, nshards=1)
+    r.set_stream(s.cuda_stream)
+    r.comm_init(rm.comm_unique_id(), 1, 0)
+    r.dispatch_frames(us[:2])
+    r.synchronize()
+    before = bytes(r.get_uniforms())
+    r.comm_set_timeout(300)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(int(6e9))  # ~2-3 s of spinning on the context's stream
+    t0 = time.monotonic()
+    with pytest.raises(rm.RMError) as e:
+        r.dispatch_frames(us)  # 8 frames: the next slot holds none yet
+    assert e.value.code == rm.RM_ERR_COMM and "did not complete within 300 ms" in str(e.value)
+    assert time.monotonic() - t0 < 30.0
+    assert bytes(r.get_uniforms()) == before
+    s.synchronize()
+    r.close()
+
+
 def test_batch_timing_and_phases(rm, gpu):
     W, H = 160, 90
     us = _frames(rm, 6)
@@ -243,3 +308,63 @@ def test_batch_gather_layout_assembles(rm, gpu, N, R, R0, n):
             np.testing.assert_array_equal(frame.cpu().numpy(), ref[k][0], err_msg=f"frame {k}")
         with pytest.raises(rm.RMError):
             a.unshard_batch_rgba8(gathered.data_ptr(), n, n, frame.data_ptr())
+
+
+def _two_gpus(rm):
+    if rm.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+
+
+@pytest.mark.parametrize("R0", [8, 5])
+def test_batch_on_two_gpus_ngpus(rm, gpu, R0):
+    """a real two-device gather of a batch (rm_config.ngpus = 2, one
+    process): every frame of the batch on device 0 equals its one-GPU render."""
+    _two_gpus(rm)
+    W, H = 160, 90
+    us = _frames(rm, 5)
+    ref = _per_frame(rm, W, H, us)
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F, ngpus=2, row_block=8,
+                     rank0_rows=R0) as r:
+        for rep in range(2):
+            r.dispatch_frames(us)
+            _check_batch(rm, r, us, ref)
+
+
+def test_batch_on_two_ranks_comm_init(rm, gpu):
+    """two rm_comm_init ranks on two devices (one thread each, the
+    calls are collective): rank 0 reads every assembled frame of the batch, rank 1
+    (the non-root branch of batch_finish and read_frame) its shard of every frame."""
+    import threading
+    _two_gpus(rm)
+    W, H, R, R0 = 160, 90, 8, 6
+    us = _frames(rm, 4)
+    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
+    cid = rm.comm_unique_id()
+    got, errs = {}, []
+
+    def rank(r):
+        try:
+            with rm.Renderer(W, H, row_block=R, shard=r, nshards=2, rank0_rows=R0, device=r) as c:
+                c.comm_init(cid, 2, r)
+                for rep in range(2):
+                    c.dispatch_frames(us)
+                    got[(r, rep)] = [c.read_frame_rgba8(k) for k in range(len(us))]
+                    got[(r, rep, "last")] = c.read_rgba8()
+        except Exception as e:  # reported by the main thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    rows1 = rm.shard_global_rows(H, R, 1, 2, R0)
+    real1 = rows1[rows1 >= 0]
+    for rep in range(2):
+        for k in range(len(us)):
+            np.testing.assert_array_equal(got[(0, rep)][k], ref[k][0], err_msg=f"rank 0 frame {k}")
+            np.testing.assert_array_equal(got[(1, rep)][k][: len(real1)], ref[k][0][real1],
+                                          err_msg=f"rank 1 shard of frame {k}")
+        np.testing.assert_array_equal(got[(0, rep, "last")], ref[-1][0])
+        np.testing.assert_array_equal(got[(1, rep, "last")][: len(real1)], ref[-1][0][real1])

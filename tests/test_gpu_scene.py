@@ -316,6 +316,22 @@ def test_specialised_far_camera_uses_generic(rm, gpu):
             np.testing.assert_array_equal(r.read_rgba32f(), want[k])
 
 
+@pytest.mark.parametrize("lx", [1e15, 1e30, 3e38])
+def test_specialised_far_light_equals_generic(rm, gpu, lx):
+    """the light position is a free uniform and shadow rays are
+    light - pos, unnormalised (glsl:184, 235), so with a light near FLT_MAX shadow
+    points overflow.  The specialised kernels' shadow march takes the full-range
+    sqrt (as the generic kernel), so far lights, inf and NaN included, render the
+    generic kernel's image bit for bit (camera near: the specialised kernels run)."""
+    for scene in (rm.default_scene(), floor_last_scene(rm, 2)):
+        for sm in (0, 1):
+            u = rm.sweep_uniforms(60, 120, 3, True, sm)
+            u.light.position[0] = lx
+            u.light.position[1] = lx / 3
+            _same(_render_spec(rm, u, 64, 48, scene, counters=False),
+                  _render(rm, u, 64, 48, scene=scene, counters=False))
+
+
 def test_specialise_toggle_and_graph(rm, gpu):
     """Toggling specialisation and switching tables re-captures the graph."""
     a, b = rm.default_scene(), random_scene(rm, 7)
