@@ -298,6 +298,12 @@ int rm_scene_specialize(rm_ctx *ctx, int enable);
  * no scratch), or 0 when the generic table kernel (or the built-in scene)
  * renders; a table that spills at 6 waves is not specialised. */
 int rm_scene_kernel_waves(const rm_ctx *ctx, int32_t *waves);
+/* Diagnostics (API version 5): the table as rm_set_scene compiles it on the host
+ * for the device (no device needed): the n entries' words, then the exit header
+ * with the bounds of the provable exits and the culling balls.  *nwords = its
+ * length; words == NULL queries the length only.  RM_ERR_INVALID (with the
+ * reason in rm_last_error(NULL)) for a table rm_set_scene would refuse. */
+int rm_scene_compile(const rm_primitive *prims, int32_t n, uint32_t *words, size_t capacity, size_t *nwords);
 /* Diagnostics: the code object rm_scene_specialize would load for this table
  * on `arch` (e.g. "gfx950"), compiled without a device.  *size = its size;
  * out == NULL queries the size only; *size = 0: the table is not specialised

@@ -1788,6 +1788,22 @@ int rm_set_scene(rm_ctx* c, const rm_primitive* prims, int32_t n) {
   return RM_OK;
 }
 
+int rm_scene_compile(const rm_primitive* prims, int32_t n, uint32_t* words, size_t capacity, size_t* nwords) {
+  if (!nwords) return fail(nullptr, RM_ERR_INVALID, "rm_scene_compile: null nwords");
+  *nwords = 0;
+  if (n < 1 || n > RM_MAX_PRIMITIVES)
+    return fail(nullptr, RM_ERR_INVALID, "rm_scene_compile: need 1..RM_MAX_PRIMITIVES primitives");
+  std::vector<uint32_t> w(rm::scene_words(n));
+  const char* why = "rm_scene_compile: bad table";
+  if (rm::compile_scene(prims, n, w.data(), &why) != RM_OK) return fail(nullptr, RM_ERR_INVALID, why);
+  *nwords = w.size();
+  if (words) {
+    if (capacity < w.size()) return fail(nullptr, RM_ERR_INVALID, "rm_scene_compile: capacity < *nwords");
+    std::memcpy(words, w.data(), w.size() * sizeof(uint32_t));
+  }
+  return RM_OK;
+}
+
 int rm_scene_specialize(rm_ctx* c, int enable) {
   if (!c) return RM_ERR_INVALID;
   for (rm_ctx* s : c->subs) {

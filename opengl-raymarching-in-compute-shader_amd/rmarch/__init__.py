@@ -135,6 +135,18 @@ def default_scene() -> list:
     return [out[i] for i in range(n.value)]
 
 
+def scene_words(prims: Sequence[rm_primitive]) -> np.ndarray:
+    """The table as rm_set_scene compiles it for the device (rm_scene_compile; host only):
+    uint32 words, the entries then the exit header (csrc/rm_internal.hpp)."""
+    n = len(prims)
+    tbl = (rm_primitive * max(n, 1))(*prims)
+    nw = C.c_size_t(0)
+    _check(lib().rm_scene_compile(tbl, n, None, 0, C.byref(nw)))
+    out = (C.c_uint32 * nw.value)()
+    _check(lib().rm_scene_compile(tbl, n, out, nw.value, C.byref(nw)))
+    return np.frombuffer(out, np.uint32).copy()
+
+
 # GLFW key / action codes (glfw3.h) and held-key bits, as in include/rm_api.h
 KEY_A, KEY_D, KEY_L, KEY_S, KEY_W = 65, 68, 76, 83, 87
 KEY_ESCAPE, KEY_DOWN, KEY_UP, KEY_F1 = 256, 264, 265, 290
@@ -213,6 +225,8 @@ _SIGS = {
     "rm_get_scene": (C.c_int, [_P, C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_int32)]),
     "rm_scene_specialize": (C.c_int, [_P, C.c_int]),
     "rm_scene_kernel_waves": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "rm_scene_compile": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.POINTER(C.c_uint32),
+                                   C.c_size_t, C.POINTER(C.c_size_t)]),
     "rm_jit_code_object": (C.c_int, [C.POINTER(rm_primitive), C.c_int32, C.c_char_p, C.c_void_p,
                                      C.c_size_t, C.POINTER(C.c_size_t)]),
     "rm_sweep_uniforms": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,

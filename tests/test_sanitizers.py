@@ -1,0 +1,54 @@
+"""The CPU suite's host-logic tests under AddressSanitizer + UndefinedBehaviorSanitizer
+(VERDICT r04 #7).
+
+`make asan` builds librm with the sanitizers on its host code (the C-ABI and
+its argument checks, the table compiler rm::compile_scene / rm::exit_bounds fed
+arbitrary user tables, the by-name uniform lookup, input replay, the shard map,
+the hiprtc driver) and the oracle, every report fatal.  This test runs the
+host-logic test files in a child pytest against those builds (clang's ASan
+runtime preloaded into the Python process, RM_LIBRM / RM_ORACLE pointing at
+them): any heap overflow, use after free or undefined behaviour fails it.  The
+table compiler also gets a hypothesis fuzz there (tests/test_fuzz_tables.py).
+GPU sanitizers are not available; the device code is the production build's."""
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm"
+HOST_TESTS = ["test_abi.py", "test_shard.py", "test_scene_table.py", "test_input.py",
+              "test_camera_goldens.py", "test_cull_bounds.py", "test_oracle_kats.py",
+              "test_goldens.py", "test_fuzz_tables.py", "test_bench_config.py"]
+
+
+def _asan_runtime():
+    rt = sorted(glob.glob(os.path.join(LLVM, "lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")))
+    return rt[-1] if rt else None
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") or _asan_runtime() is None,
+                    reason="hipcc / clang's ASan runtime not installed")
+def test_host_code_is_sanitizer_clean():
+    r = subprocess.run(["make", "-s", "-j8", "asan"], cwd=ROOT, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ)
+    env.update(LD_PRELOAD=_asan_runtime(),
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:strict_string_checks=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               RM_LIBRM=os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd", "build", "asan",
+                                     "librm.so"),
+               RM_ORACLE=os.path.join(ROOT, "oracle", "_build", "librm_oracle_asan.so"))
+    # (test_table_compiles_once repeats test_table_specialises_without_a_device's
+    # hiprtc path, ~1 min under the sanitizers: one of the two runs here)
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "not gpu", "-p", "no:cacheprovider",
+           "-k", "not test_table_compiles_once"]
+    cmd += [os.path.join(ROOT, "tests", t) for t in HOST_TESTS]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1500)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-6000:]
+    assert "runtime error" not in out and "ERROR: AddressSanitizer" not in out, out[-6000:]
+    # the child really ran against the sanitizer builds
+    assert " passed" in r.stdout
