@@ -594,10 +594,10 @@ def main() -> int:
             cnt_total = dict(c) if cnt_total is None else {x: cnt_total[x] + c[x] for x in c}
     mean_kernel_ms = kernel_ms / max(launches, 1)
     kname = "k_sample" if cfg["aa"] else "k_pixel"
-    if batched and scene is None:
-        kname += "_frames"  # the batched kernels (grid.z = frame); PMC values per frame
     if scene is not None:
         kname = "k_table_sample" if cfg["aa"] else "k_table_pixel"
+    if batched:
+        kname += "_frames"  # the batched kernels (grid.z = frame); PMC values per frame
     pmc, traffic_src = pmc_entry(kname if kname.endswith("_frames") else kname + "<false>",
                                  f"cfg{args.config}" + ("-spec" if spec else ""))
     traffic = int(pmc["hbm_bytes_per_launch"]) if pmc else None

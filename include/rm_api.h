@@ -199,9 +199,11 @@ int rm_dispatch(rm_ctx *ctx);
  * shards of the n frames in one launch, one ncclGather moves all n shards, and
  * rank 0 assembles the n frames; the gather runs on a second stream of the
  * context, so the next batch renders while this one gathers (a consumer on the
- * caller's own stream orders itself after it with rm_wait_output).  Frames with a
- * different AA setting render in separate launches; a runtime scene table
- * renders one launch per frame.  Not available with cfg.counters. */
+ * caller's own stream orders itself after it with rm_wait_output).  A runtime
+ * scene table's frames batch the same way (API version 5; its specialised
+ * kernels too).  Frames with a different AA setting, or (specialised tables) a
+ * camera that needs the generic kernel, render in separate launches.  Not
+ * available with cfg.counters. */
 #define RM_MAX_BATCH 32
 int rm_dispatch_frames(rm_ctx *ctx, const rm_uniforms *frames, int32_t n);
 /* Wait for all work queued on the context (== glMemoryBarrier + the

@@ -24,6 +24,7 @@ namespace rm {
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
 hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy);
+hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, bool slazy);
 bool table_slazy(const uint32_t* words, int32_t n);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
@@ -1237,16 +1238,20 @@ int ensure_ring(rm_ctx* c, int n, int rows) {
 }
 
 // The frame constants of frames[0..n) with their output pointers, launched in
-// runs of one AA setting (one grid per run); a runtime scene table renders one
-// launch per frame.  out8(k) / out32(k): frame k's destinations.
+// runs of one kernel: one AA setting, and for a runtime scene table one of its
+// kernels (the specialised ones, or the generic one for a frame frame_jit
+// refuses); one grid per run.  out8(k) / out32(k): frame k's destinations.
 // (C++ linkage: this block sits inside the C-ABI's extern "C")
 extern "C++" template <class O8, class O32>
 int launch_batch(rm_ctx* c, const rm_uniforms* u, int n, O8 out8, O32 out32) {
-  static thread_local rmd::FrameBatch B;  // 11.5 KB of kernel arguments
+  static thread_local rmd::FrameBatch B;  // 11.9 KB of kernel arguments
   int m = 0;
+  const rm::JitTable* run_jit = nullptr;  // the run's table kernels: specialised, or null = generic
   auto flush = [&]() -> int {
     if (m == 0) return RM_OK;
-    const hipError_t e = rm::launch_frames(B, m, c->stream);
+    const hipError_t e = !c->nprims ? rm::launch_frames(B, m, c->stream)
+                         : run_jit ? rm::launch_table_jit_frames(run_jit, B, m, c->stream)
+                                   : rm::launch_table_frames(B, m, c->stream, table_slots(c), table_sl(c));
     m = 0;
     if (e != hipSuccess) return hip_fail(c, e, "batch launch");
     return RM_OK;
@@ -1259,14 +1264,9 @@ int launch_batch(rm_ctx* c, const rm_uniforms* u, int n, O8 out8, O32 out32) {
     F.rgba32f = out32(k);
     F.sdf_counts = nullptr;
     F.counters = nullptr;
-    if (c->nprims) {
-      const rm::JitTable* jit = frame_jit(c, F);
-      const hipError_t e = jit ? rm::launch_table_jit(jit, F, false, c->stream)
-                               : rm::launch_table(F, false, c->stream, table_slots(c), table_sl(c));
-      if (e != hipSuccess) return hip_fail(c, e, "kernel launch");
-      continue;
-    }
-    if (m > 0 && B.f[0].aa != F.aa && (rc = flush()) != RM_OK) return rc;
+    const rm::JitTable* jit = c->nprims ? frame_jit(c, F) : nullptr;
+    if (m > 0 && (B.f[0].aa != F.aa || jit != run_jit) && (rc = flush()) != RM_OK) return rc;
+    run_jit = jit;
     B.f[m++] = F;
   }
   return flush();

@@ -50,8 +50,10 @@ namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, rm::JitTable*> g_cache;
 
-const char* const kNames[2][2] = {{"rmd::k_table_pixel<false>", "rmd::k_table_pixel<true>"},
-                                  {"rmd::k_table_sample<false>", "rmd::k_table_sample<true>"}};
+// [aa][counters] as JitTable::fn, then the batch kernels [aa] (JitTable::fnb)
+const char* const kNames[3][2] = {{"rmd::k_table_pixel<false>", "rmd::k_table_pixel<true>"},
+                                  {"rmd::k_table_sample<false>", "rmd::k_table_sample<true>"},
+                                  {"rmd::k_table_pixel_frames<>", "rmd::k_table_sample_frames<>"}};
 }  // namespace
 
 namespace rm {
@@ -171,14 +173,15 @@ int jit_compile_waves(const uint32_t* words, int32_t n, const std::string& arch,
   return RM_OK;
 }
 
-// Waves per SIMD the production kernels (k_table_*<false>; lowered[0],
-// lowered[2]) of a compiled code object run at, or 0 when either needs scratch;
+// Waves per SIMD the production kernels (k_table_*<false>, lowered[0] and [2],
+// and the batch kernels, [4] and [5]) of a compiled code object run at, or 0
+// when any needs scratch;
 // -1 (with err) when a descriptor is missing: that is an error, not a spill, as
 // silently falling back to the generic kernel would hide a code-object layout
 // change.
 int production_waves(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
   int w = 8;
-  for (int k : {0, 2}) {
+  for (int k : {0, 2, 4, 5}) {
     long priv = -1;
     int vg = 0;
     if (!kernel_desc(c, l[k], &priv, &vg)) {
@@ -196,7 +199,7 @@ int production_waves(const std::vector<char>& c, const std::vector<std::string>&
 // err) when a descriptor is missing.
 long production_scratch(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
   long most = 0;
-  for (int k : {0, 2}) {
+  for (int k : {0, 2, 4, 5}) {
     long priv = -1;
     int vg = 0;
     if (!kernel_desc(c, l[k], &priv, &vg)) {
@@ -303,6 +306,8 @@ int jit_table(const uint32_t* words, int32_t n, const JitTable** out, std::strin
   hipError_t e = hipModuleLoadData(&j->mod, code.data());
   for (int k = 0; k < 4 && e == hipSuccess; ++k)
     e = hipModuleGetFunction(&j->fn[k / 2][k % 2], j->mod, lowered[k].c_str());
+  for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    e = hipModuleGetFunction(&j->fnb[k], j->mod, lowered[4 + k].c_str());
   if (e != hipSuccess) {
     if (j->mod) (void)hipModuleUnload(j->mod);
     delete j;
@@ -321,6 +326,15 @@ hipError_t launch_table_jit(const JitTable* j, const rmd::Frame& F, bool counter
                                  args, nullptr);
   return hipModuleLaunchKernel(j->fn[0][counters], (F.width + 7) / 8, (F.rows + 7) / 8, 1, 64, 1, 1, 0, s, args,
                                nullptr);
+}
+
+hipError_t launch_table_jit_frames(const JitTable* j, const rmd::FrameBatch& B, int n, hipStream_t s) {
+  if (n < 1 || n > rmd::kMaxBatch) return hipErrorInvalidValue;
+  const rmd::Frame& F = B.f[0];
+  void* args[] = {const_cast<rmd::FrameBatch*>(&B)};
+  if (F.aa)
+    return hipModuleLaunchKernel(j->fnb[1], (F.width + 3) / 4, (F.rows + 3) / 4, n, 64, 1, 1, 0, s, args, nullptr);
+  return hipModuleLaunchKernel(j->fnb[0], (F.width + 7) / 8, (F.rows + 7) / 8, n, 64, 1, 1, 0, s, args, nullptr);
 }
 
 }  // namespace rm

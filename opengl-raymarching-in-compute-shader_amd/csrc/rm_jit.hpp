@@ -9,6 +9,7 @@
 
 namespace rmd {
 struct Frame;
+struct FrameBatch;
 }
 
 namespace rm {
@@ -19,6 +20,7 @@ namespace rm {
 struct JitTable {
   hipModule_t mod = nullptr;
   hipFunction_t fn[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  hipFunction_t fnb[2] = {nullptr, nullptr};  // k_table_{pixel,sample}_frames: batches [aa]
   int waves = 0;  // the register bound compiled for (waves per SIMD, rm_jit.hip)
 };
 
@@ -28,5 +30,7 @@ struct JitTable {
 int jit_table(const uint32_t* words, int32_t n, const JitTable** out, std::string& err);
 // The same grid and block as launch_table (rm_table.hip); no dynamic LDS.
 hipError_t launch_table_jit(const JitTable* j, const rmd::Frame& F, bool counters, hipStream_t s);
+// n frames of one batch (rm_dispatch_frames): grid.z = the frame.
+hipError_t launch_table_jit_frames(const JitTable* j, const rmd::FrameBatch& B, int n, hipStream_t s);
 
 }  // namespace rm

@@ -416,6 +416,30 @@ __device__ __forceinline__ float table_exit_T(const float* ex, float c, float hm
 // KL: the slots this instance holds (>= the table's EX_NSLOTS; launch_table
 // picks the generic kernel's instance from the table, a specialised table's
 // unrolled loops fold the unused slots away).
+// The first expiry of slot j of a march that starts without the host's step 0
+// (reflected and shadow marches): -inf (re-test at the first step) for the
+// table's ns slots, +inf (never) for an instance's unused ones.  In a
+// specialised kernel ns is a compile-time count and this folds to a constant.
+// In the generic kernel ns is the table's, at run time; the select there is
+// formed in scalar registers where the march starts (volatile: LLVM had hoisted
+// the KL uniform selects out of the bounce loop into VGPRs live across the
+// whole kernel, 5 of them spilled in the reference-shaped instance, round 5).
+__device__ __forceinline__ float slot_init(int j, int ns) {
+#ifdef RM_TABLE_STATIC
+  return j < ns ? -__builtin_huge_valf() : __builtin_huge_valf();
+#else
+  uint32_t b;
+  asm volatile(
+      "s_mov_b32 %0, 0x7f800000\n\t"
+      "s_cmp_gt_i32 %1, %2\n\t"
+      "s_cselect_b32 %0, 0xff800000, %0"
+      : "=&s"(b)
+      : "s"(__builtin_amdgcn_readfirstlane(ns)), "i"(j)
+      : "scc");
+  return __uint_as_float(b);
+#endif
+}
+
 template <int KL>
 struct TLazy {
   const float* ex;
@@ -432,7 +456,7 @@ struct TLazy {
     const uint32_t all = S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u;
     always = ns > 0 ? __float_as_uint(ex[rm::EX_EVAL_MASK]) : all;
 #pragma unroll
-    for (int j = 0; j < KL; ++j) te(j) = j < ns ? -INF : INF;
+    for (int j = 0; j < KL; ++j) te(j) = slot_init(j, ns);
     temin = ns > 0 ? -INF : INF;
     const float lip = ex[rm::EX_LIP];
     sig2 = 2.0f * ex[rm::EX_SIGMA];
@@ -633,7 +657,6 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   }
   float t = 0.0f, dl = 0.0f;
   int i0 = 1;  // sdf evaluations the first loop step brings the count to
-  const float NEG = -__builtin_huge_valf();
   if (prep && prep[rm::TP_VALID] != 0.0f) {
     // step 0 at the camera, evaluated on the host (tmarch above); the gaps are
     // TLazy's, their expiries at TLazy's rate
@@ -644,7 +667,7 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
     i0 = 2;
   } else {
     #pragma unroll
-    for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? NEG : __builtin_huge_valf();
+    for (int j = 0; j < KL; ++j) lz.te[j] = slot_init(j, ns);
   }
   lz.temin = slot_min(lz.te, ns);
   if (!(t <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
@@ -1022,10 +1045,25 @@ __device__ __forceinline__ void flush_counts(const Frame& F, const TCnt& c) {
 #define RM_TABLE_SL_WAVES 7
 #endif
 
+// The lane id re-formed after the march (v_mbcnt, one-wave workgroups: the same
+// value as threadIdx.x): the output pixel's coordinates and index come from it
+// instead of staying live across trender, where both table kernels spilled them
+// to scratch (5 VGPRs, round 5).  Volatile so that LLVM cannot fold it back onto
+// the prologue's threadIdx.x.
+__device__ __forceinline__ int out_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+// Index in the launch's [rows][width] image of pixel (tx, ty) of tile (bx, by)
+// of `edge` x `edge` pixels.
+__device__ __forceinline__ size_t out_index(const Frame& F, int tx, int ty, int edge, int bx, int by) {
+  return (size_t)(by * edge + ty) * (size_t)F.width + (size_t)(bx * edge + tx);
+}
+
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
-__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
-  extern __shared__ float lds[];
+template <bool COUNT, int KL, bool SL>
+__device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x;
   const int by = tile_row(blockIdx.y, gridDim.y);
@@ -1044,9 +1082,10 @@ __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) vo
   cast_ray(F, lane_uv(F, 0, px, -1), lane_uv(F, 1, py, -1), ro, rd);
   if (COUNT) c.rays++;
   const f3 col = trender<COUNT, KL, SL>(F, S, ro, rd, c);
-  store_pixel(F, idx, col.x, col.y, col.z, 1.0f);
+  const size_t at = out_index(F, out_lane() & 7, out_lane() >> 3, 8, bx, by);
+  store_pixel(F, at, col.x, col.y, col.z, 1.0f);
   if (COUNT) {
-    F.sdf_counts[idx] = c.march + c.reflect + c.shadow + 4u * c.normals;
+    F.sdf_counts[at] = c.march + c.reflect + c.shadow + 4u * c.normals;
     flush_counts(F, c);
   }
 }
@@ -1054,9 +1093,8 @@ __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) vo
 // main glsl:291-344 with 4x supersampling: one lane per (pixel, sample), the 4
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
-__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
-  extern __shared__ float lds[];
+template <bool COUNT, int KL, bool SL>
+__device__ __forceinline__ void table_sample_body(const Frame& F, float* lds) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
   const int by = tile_row(blockIdx.y, gridDim.y);
@@ -1083,15 +1121,49 @@ __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) vo
     cnt = mine + __shfl(mine, lane + 1) + __shfl(mine, lane + 2) + __shfl(mine, lane + 3);
     flush_counts(F, c);
   }
-  if (s != 0) return;
-  if (py >= 0) {
+  // the pixel's coordinates and index re-formed from the lane id (not kept
+  // across the march: see out_lane)
+  const int ol = out_lane();
+  if ((ol & 3) != 0) return;
+  const size_t at = out_index(F, (ol >> 2) & 3, ol >> 4, 4, bx, by);
+  if (global_row(F, by * 4 + (ol >> 4)) >= 0) {
     const float o0 = ((col.x + r1) + r2) + r3, o1 = ((col.y + g1) + g2) + g3,
                 o2 = ((col.z + b1) + b2) + b3;
-    store_pixel(F, idx, o0 / 4.0f, o1 / 4.0f, o2 / 4.0f, 1.0f);
+    store_pixel(F, at, o0 / 4.0f, o1 / 4.0f, o2 / 4.0f, 1.0f);
   } else {
-    store_pixel(F, idx, 0.0f, 0.0f, 0.0f, 0.0f);
+    store_pixel(F, at, 0.0f, 0.0f, 0.0f, 0.0f);
   }
-  if (COUNT) F.sdf_counts[idx] = cnt;
+  if (COUNT) F.sdf_counts[at] = cnt;
+}
+
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
+  extern __shared__ float lds[];
+  table_pixel_body<COUNT, KL, SL>(F, lds);
+}
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
+  extern __shared__ float lds[];
+  table_sample_body<COUNT, KL, SL>(F, lds);
+}
+
+// Frame batches (rm_dispatch_frames): n frames of one table,
+// size and AA setting in one launch, grid.z = the frame, each workgroup reading
+// its frame's constants from the batch in the kernel arguments (as
+// k_sample_frames, rm_kernels.hip).  The bodies are the kernels' above, so every
+// frame is the image of its own dispatch.  Production kernels only (a batch
+// collects no counters).
+template <int KL = rm::EX_MAX_SLOTS, bool SL = false>
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel_frames(
+    FrameBatch B) {
+  extern __shared__ float lds[];
+  table_pixel_body<false, KL, SL>(B.f[blockIdx.z], lds);
+}
+template <int KL = rm::EX_MAX_SLOTS, bool SL = false>
+__global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample_frames(
+    FrameBatch B) {
+  extern __shared__ float lds[];
+  table_sample_body<false, KL, SL>(B.f[blockIdx.z], lds);
 }
 
 }  // namespace rmd
@@ -1118,7 +1190,33 @@ void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
       hipLaunchKernelGGL((rmd::k_table_pixel<false, KL, SL>), g, dim3(64), lds, s, F);
   }
 }
+
+template <int KL, bool SL>
+void launch_table_frames_kl(const rmd::FrameBatch& B, int n, hipStream_t s) {
+  const rmd::Frame& F = B.f[0];
+  const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
+  if (F.aa)
+    hipLaunchKernelGGL((rmd::k_table_sample_frames<KL, SL>), dim3((F.width + 3) / 4, (F.rows + 3) / 4, n), dim3(64),
+                       lds, s, B);
+  else
+    hipLaunchKernelGGL((rmd::k_table_pixel_frames<KL, SL>), dim3((F.width + 7) / 8, (F.rows + 7) / 8, n), dim3(64),
+                       lds, s, B);
+}
 }  // namespace
+
+// The frames B.f[0..n) of one table, size and AA setting in one launch: the
+// generic kernel's instance for the table (launch_table below).
+hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, bool slazy) {
+  if (n < 1 || n > rmd::kMaxBatch) return hipErrorInvalidValue;
+  if (nslots <= TABLE_FEW_SLOTS) {
+    if (slazy) launch_table_frames_kl<TABLE_FEW_SLOTS, true>(B, n, s);
+    else launch_table_frames_kl<TABLE_FEW_SLOTS, false>(B, n, s);
+  } else {
+    if (slazy) launch_table_frames_kl<rm::EX_MAX_SLOTS, true>(B, n, s);
+    else launch_table_frames_kl<rm::EX_MAX_SLOTS, false>(B, n, s);
+  }
+  return hipGetLastError();
+}
 
 // nslots: the table's lazy slots (EX_NSLOTS of its compiled words).  Tables with
 // at most TABLE_FEW_SLOTS of them (the reference scene has 5) take an instance

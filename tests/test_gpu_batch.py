@@ -107,18 +107,75 @@ def test_batch_sharded_and_external_output(rm, gpu):
         np.testing.assert_array_equal(r.read_frame_rgba8(1), ref[1][0])
 
 
-@pytest.mark.parametrize("spec", [False, True])
-def test_batch_scene_table(rm, gpu, spec):
-    """A runtime scene table renders a batch one launch per frame: same images."""
-    W, H = 128, 72
-    us = _frames(rm, 4)
-    ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
-    with rm.Renderer(W, H) as r:
+def _tables(rm):
+    from test_gpu_scene import floor_last_scene, random_scene
+    return {"reference": rm.default_scene(), "floor": floor_last_scene(rm, 3),
+            "random": random_scene(rm, 5)}
+
+
+@pytest.mark.parametrize("spec", [False, True], ids=["generic", "specialised"])
+@pytest.mark.parametrize("table", ["reference", "floor", "random"])
+@pytest.mark.parametrize("n,aa", [(1, True), (5, True), (32, False), (13, False)])
+def test_batch_scene_table(rm, gpu, spec, table, n, aa):
+    """a runtime scene table renders a batch in one launch
+    (k_table_*_frames, grid.z = the frame; the hiprtc-specialised ones too): every
+    frame byte-equal to its own rm_dispatch (RGBA32F bit-equal)."""
+    W, H = 96, 54
+    sc = _tables(rm)[table]
+    us = _frames(rm, n, b=2 if aa else 1, aa=aa)
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as one:
+        if spec:
+            one.specialize_scene(True)
+        one.set_scene(sc)
+        ref = []
+        for u in us:
+            one.dispatch(u)
+            ref.append((one.read_rgba8(), one.read_rgba32f()))
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as r:
         if spec:
             r.specialize_scene(True)
-        r.set_scene(rm.default_scene())
+        r.set_scene(sc)
+        r.enable_timing(True)
+        r.kernel_time_ms(reset=True)
         r.dispatch_frames(us)
+        _, launches = r.kernel_time_ms(reset=True)
+        assert launches == n  # one timed launch counting its n frames
         _check_batch(rm, r, us, ref)
+
+
+def test_batch_scene_table_mixed_kernels(rm, gpu):
+    """A specialised table's batch whose frames need different kernels (a camera
+    beyond 1e15 renders with the generic kernel, rm_api.hip frame_jit) and both AA
+    settings: runs of one kernel each, every frame equal to its own dispatch."""
+    W, H = 64, 40
+    us = _frames(rm, 6)
+    far = _frames(rm, 1)[0]
+    far.camera.pos[0] = 3e15
+    us = us[:2] + [far] + us[2:4] + _frames(rm, 2, b=1, aa=False)
+    with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8 | rm.RM_OUT_RGBA32F) as one:
+        one.specialize_scene(True)
+        one.set_scene(rm.default_scene())
+        ref = []
+        for u in us:
+            one.dispatch(u)
+            ref.append((one.read_rgba8(), one.read_rgba32f()))
+        one.dispatch_frames(us)
+        _check_batch(rm, one, us, ref)
+
+
+def test_batch_scene_table_matches_oracle(rm, oracle, gpu):
+    """A table batch (generic kernel, reference-shaped and random tables) against the
+    oracle's table mode: every frame within 1 LSB."""
+    W, H = 64, 40
+    for name, sc in _tables(rm).items():
+        us = _frames(rm, 3, b=2)
+        with rm.Renderer(W, H) as r:
+            r.set_scene(sc)
+            r.dispatch_frames(us)
+            for k, u in enumerate(us):
+                ref = oracle.render(u, W, H, scene=sc, want_counts=False)["rgba8"]
+                d = np.abs(r.read_frame_rgba8(k).astype(int) - ref.astype(int))
+                assert d.max() <= 1, (name, k, d.max())
 
 
 @pytest.mark.parametrize("form", ["comm_init", "ngpus"])

@@ -124,6 +124,10 @@ STRESS = [
     ("cam_in_blend", None, (-5.0, 0.0, -10.0)),
     ("cam_below_floor", None, (0.0, -8.0, 15.0)),
     ("cam_far", None, (40.0, 30.0, 120.0)),
+    # floor hits beyond the int range: checkers' int() saturates
+    ("cam_x_3e9", None, (3.0e9, 0.0, 15.0)),
+    ("cam_x_-3e9", None, (-3.0e9, 0.0, 15.0)),
+    ("cam_z_3e9", None, (0.0, 0.0, 3.0e9)),
 ]
 
 

@@ -34,6 +34,17 @@ def test_checkers_colour(oracle, U):                         # glsl:77-80
     assert oracle.sdf(U, (201.5, 0.0, 201.5)).color[0] == pytest.approx(0.2)
 
 
+def test_checkers_int_saturates(oracle, U):                  # glsl:79, DESIGN.md §2
+    # int() of a value beyond the int range: GLSL leaves it undefined; the
+    # contract takes gfx950's v_cvt_i32_f32 (saturating, NaN -> 0): int(1000 +
+    # 3e9) = INT_MAX (odd), int(1000 - 3e9) = INT_MIN (even)
+    assert oracle.sdf(U, (3.0e9, 0.0, 200.5)).color[0] == 1.0
+    assert oracle.sdf(U, (3.0e9, 0.0, 201.5)).color[0] == pytest.approx(0.2)
+    assert oracle.sdf(U, (-3.0e9, 0.0, 200.5)).color[0] == pytest.approx(0.2)
+    assert oracle.sdf(U, (-3.0e9, 0.0, 201.5)).color[0] == 1.0
+    assert oracle.sdf(U, (3.0e9, 0.0, 3.0e9)).color[0] == pytest.approx(0.2)
+
+
 def test_blend_follows_itime(rm, oracle):                    # glsl:115-117
     # at the box/sphere centre both sdfs are negative: box -2.5, sphere -3
     for it in (0.0, 1.0, 2.5):

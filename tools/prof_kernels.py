@@ -4,10 +4,10 @@
 KIND: pixel | table | table-spec.  The frames are bench.py's own
 (bench_frames(STEPS): step k renders sweep frame floor(k * 120 / STEPS)), one
 launch each, so the per-launch PMC means describe the benched workload.  BATCH >
-1 (pixel only): the same frames once more as rm_dispatch_frames batches of
-BATCH frames (k_pixel_frames / k_sample_frames, the kernels bench.py times for
-that configuration); tools/summarize_profiles.py divides their per-launch
-counters by BATCH.
+1: the same frames once more as rm_dispatch_frames batches of BATCH frames
+(k_pixel_frames / k_sample_frames, or a table's k_table_*_frames: the kernels
+bench.py times for that configuration); tools/summarize_profiles.py divides
+their per-launch counters by BATCH.
 """
 import os
 import sys
@@ -32,7 +32,7 @@ with rm.Renderer(cfg["width"], cfg["height"], kernel=k) as r:
     for u in us:
         r.dispatch(u)
     r.synchronize()
-    if batch > 1 and kname == "pixel":
+    if batch > 1:
         for i in range(0, len(us), batch):
             r.dispatch_frames(us[i:i + batch])
         r.synchronize()
