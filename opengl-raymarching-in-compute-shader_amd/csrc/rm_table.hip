@@ -733,7 +733,10 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
     // hit step's distance is its value; otherwise the block ran at this step and
     // idb is its winner (lazy_id, rm_scene.hpp)
     const f3 p = add(ro, muls(rd, t));
-    const int k = dl != plane(p.y) ? lz.idb : kp;
+    int k = dl != plane(p.y) ? lz.idb : kp;
+    // the winner as a 32-bit index here: LLVM otherwise carried its zero-extended
+    // 64-bit table offset through the bounce loop, in scratch (round 5)
+    asm volatile("" : "+v"(k));
     return THit{t, S.id(k), S.material(k), S.color(k, p), dl};
   }
   return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
