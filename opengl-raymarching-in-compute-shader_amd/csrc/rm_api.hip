@@ -23,9 +23,9 @@
 namespace rm {
 void pixel_grid(int width, int rows, bool aa, int32_t* gx, int32_t* gy);
 hipError_t launch_pixel(const rmd::Frame& F, bool counters, hipStream_t s);
-hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy);
-hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, bool slazy);
-bool table_slazy(const uint32_t* words, int32_t n);
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, int shape);
+hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, int shape);
+int table_shape(const uint32_t* words, int32_t n);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
                           int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
 hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
@@ -357,7 +357,12 @@ void prep_host(const float cam[3], float blend, float omblend, float out[16]) {
   for (int k = 0; k < 5; ++k) {
     // the gaps of scene_lazy's re-test at the camera with U = d0, in its float
     // operations: g = (lb - d0) - slack, plane gap lb - pl
-    const float lb = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+    float lb = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
+    if (k == 3) {  // the torus's own bound (rm_scene.hpp torus_lb), IEEE sqrt within its margins
+      const float r = std::sqrt(cx2 + ay2);
+      const float a = std::fmax(std::fma(r, -0x1p-12f, std::fabs(r - 2.5f)), 0.0f);
+      lb = std::fma(std::sqrt(std::fma(a, a, tz * tz)), CULL_REL_LO, -(CULL_ABS + 0.5f));
+    }
     const float g = lb - d - sl;
     out[PREP_G + k] = g > 0.0f ? g : -INFINITY;
     out[PREP_H + k] = g > 0.0f ? lb - pl : -INFINITY;
@@ -417,15 +422,16 @@ static int table_slots(const rm_ctx* c) {
   const float* ex = reinterpret_cast<const float*>(c->scene_words.data()) + (size_t)c->nprims * rm::TABLE_WORDS;
   return (int)ex[rm::EX_NSLOTS];
 }
-// A reference-shaped table (rm_table.hip table_slazy): the generic kernel's
-// production instance with the built-in march shape.
-static bool table_sl(const rm_ctx* c) {
-  return c->nprims && rm::table_slazy(c->scene_words.data(), c->nprims);
+// The generic kernel's production march for the table (rm_table.hip
+// table_shape): 1 the built-in shape (reference-shaped tables), 2 the block
+// shape of any plane-bounded table, 0 TLazy.
+static int table_sl(const rm_ctx* c) {
+  return c->nprims ? rm::table_shape(c->scene_words.data(), c->nprims) : 0;
 }
 // Which kernel a frame renders with (the graph's key): 0 built-in, 1 + the
 // generic table kernel's instance (slots, shape).
 static int table_key(const rm_ctx* c) {
-  return c->nprims ? 1 + (table_slots(c) <= rm::TABLE_FEW_SLOTS ? 0 : 1) + (table_sl(c) ? 2 : 0) : 0;
+  return c->nprims ? 1 + (table_slots(c) <= rm::TABLE_FEW_SLOTS ? 0 : 1) + 2 * table_sl(c) : 0;
 }
 
 void table_prep_host(const uint32_t* words, int32_t n, const float cam[3], float blend, float omblend,

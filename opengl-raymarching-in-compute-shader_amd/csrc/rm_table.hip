@@ -35,6 +35,7 @@
 #include "rm_internal.hpp"
 #ifndef __HIPCC_RTC__
 #include <cstring>
+#include <type_traits>
 #endif
 #include "rm_scene.hpp"
 
@@ -583,6 +584,13 @@ __device__ __forceinline__ bool slazy_table(const Table& S) {
     if ((int)ex[rm::EX_SLOTS + j] != j) return false;  // ... slot j holding entry j
   return true;
 }
+
+// gmarch's condition (a specialised table, compile-time): valid exit bounds and
+// at least one plane.
+__device__ __forceinline__ bool glazy_table(const Table& S) {
+  const float* ex = S.exits();
+  return ex[rm::EX_VALID] != 0.0f && ex[rm::EX_NPLANES] >= 1.0f;
+}
 #endif
 
 // Expiries by TLazy's argument (above), in scene_lazy's form:
@@ -742,14 +750,178 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
 }
 
-// RayMarch glsl:125-142 / reflectedRay glsl:144-161
-template <bool COUNT, int KL, bool SL = false>
+// ---- the block shape for any plane-bounded table (round 5) ----
+// smarch needs the reference's shape (one axis-aligned plane, last, every other
+// entry in a slot).  gmarch takes any table with valid exit bounds and at least
+// one plane: several planes of any orientation anywhere in the table, and more
+// bounded entries than the slots (the untracked ones are evaluated at every
+// step, as the planes).  Per step: p(t), the always-evaluated entries (EX_EVAL_
+// MASK) into the running minimum m, the planes' minimum U among them; the block
+// when some lane's expiry passes t re-tests the due slots against U with the
+// planes' budget and evaluates an entry where its new expiry does not pass t.
+//   * budget: every plane's exact value is linear along the ray, slope
+//     dot(rd, n'_j) (EX_PLANES world normals), so U(t') <= U(t) + s_max (t' - t)
+//     with s_max the largest slope, and a slot's ball bound falls at most |rd|
+//     per unit of t: a positive gap (lb - U) - sl lasts while it shrinks at
+//     |rd| + s_max + s1 (the float error of the slopes is far inside the 2^-8
+//     added to s1, as in smarch);
+//   * the distance is exact: culled entries are strictly above the minimum;
+//   * the opU winner is taken once, at the hit: every entry evaluated at the hit
+//     point in table order (dist_mask), ties to the later entry -- the winner of
+//     the reference's sdf() at that point.
+template <int KL>
+__device__ __forceinline__ THit gmarch(const Table& S, f3 ro, f3 rd, bool reflected, const float* prep) {
+  ro = topaque(ro);
+  const float* ex = S.exits();
+  const int ns = (int)ex[rm::EX_NSLOTS];
+  const int np = (int)ex[rm::EX_NPLANES];
+  const uint32_t always = __float_as_uint(uword(ex + rm::EX_EVAL_MASK));
+  const float tmax = reflected ? 200.0f : 400.0f;
+  const int nmax = reflected ? 256 : 512;
+  const float T = table_exit_T(ex, MISS_C, 0.0f, ro, rd);
+  SLazy<KL> lz;
+  {
+    const float sig2 = 2.0f * ex[rm::EX_SIGMA];
+    const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd)) * (1.0f + 0x1p-16f);  // >= |rd|
+    const float rd1 = ((fabsf(rd.x) + fabsf(rd.y)) + fabsf(rd.z)) * (1.0f + 0x1p-16f);
+    const float ro1 = (fabsf(ro.x) + fabsf(ro.y)) + fabsf(ro.z);
+    lz.s0 = sig2 * (2.0f * ro1 + ex[rm::EX_S]) * ((1.0f + 0x1p-9f) * (1.0f + 0x1p-8f));
+    lz.s1 = sig2 * rd1 * ((1.0f + 0x1p-9f) * (1.0f + 0x1p-8f));
+    lz.inv = (1.0f - 0x1p-10f) *
+             __builtin_amdgcn_rcpf((1.0f + ex[rm::EX_LIP]) * rdl + sig2 * rd1) * (1.0f - 0x1p-16f);
+    float smax = -__builtin_huge_valf();
+    RM_TS_UNROLL
+    for (int j = 0; j < rm::EX_MAX_PLANES; ++j)
+      if (j < np) smax = fmaxf(smax, dot(rd, mk(ex[rm::EX_PLANES + 4 * j], ex[rm::EX_PLANES + 4 * j + 1],
+                                                 ex[rm::EX_PLANES + 4 * j + 2])));
+    const float ratep = (rdl + smax) + lz.s1 * (1.0f + 0x1p-8f);
+    lz.invp = ratep > 0.0f ? (1.0f - 0x1p-10f) * __builtin_amdgcn_rcpf(ratep) * (1.0f - 0x1p-16f) : 0.0f;
+  }
+  float t = 0.0f, dl = 0.0f;
+  int i0 = 1;
+  if (prep && prep[rm::TP_VALID] != 0.0f) {
+    // step 0 at the camera, evaluated on the host (table_prep_host: slot j's gap
+    // with U = the planes at the camera), at TLazy's rate as in smarch
+    #pragma unroll
+    for (int j = 0; j < KL; ++j) lz.te[j] = j < ns ? __builtin_fmaxf(prep[rm::TP_G + j] * lz.inv, 0.0f) : __builtin_huge_valf();
+    dl = prep[rm::TP_D0];
+    t = dl;
+    i0 = 2;
+  } else {
+    #pragma unroll
+    for (int j = 0; j < KL; ++j) lz.te[j] = slot_init(j, ns);
+  }
+  lz.temin = slot_min(lz.te, ns);
+  if (!(t <= T)) return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
+
+  auto step = [&](float tt) {
+    const f3 p = mk(ro.x + rd.x * tt, ro.y + rd.y * tt, ro.z + rd.z * tt);
+    float m = __builtin_huge_valf(), U = __builtin_huge_valf();
+#ifdef RM_TABLE_STATIC
+    RM_TS_UNROLL
+    for (int k = 0; k < S.n; ++k) {
+      if (!((always >> k) & 1u)) continue;
+      const float v = prim_dist<kBoundedPoints>(S.entry(k), S.type(k), p, S.blend, S.omblend);
+      m = vmin(m, v);
+      if (S.type(k) == RM_PRIM_PLANE) U = vmin(U, v);
+    }
+#else
+    if (S.fp >= 0 && always == (1u << S.fp)) {
+      m = U = S.plane_fast(p);  // one plane and every bounded entry in a slot
+    } else {
+      for (uint32_t w = always; w; w &= w - 1u) {
+        const int k = __builtin_ctz(w);
+        const int ty = S.type(k);
+        const float v = prim_dist(S.entry(k), ty, p, S.blend, S.omblend);
+        m = vmin(m, v);
+        if (ty == RM_PRIM_PLANE) U = vmin(U, v);
+      }
+    }
+#endif
+    if (wany(tt >= lz.temin)) {
+      const float sl = __builtin_fmaf(lz.s1, tt, lz.s0);
+      const float pl = U + sl;
+      // the re-tests (unrolled over the slots), then the entries some lane must
+      // evaluate (a lane whose expiry passes t takes a value proven above its
+      // minimum: m is unchanged), in one loop over their mask
+      uint32_t due = 0;
+      #pragma unroll
+      for (int j = 0; j < KL; ++j) {
+        if (j >= ns || !wany(tt >= lz.te[j])) continue;
+#ifdef RM_TABLE_STATIC
+        const float* B = S.entry((int)ex[rm::EX_SLOTS + j]) + rm::TW_BALL;
+#else
+        const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];  // the slot's ball, staged
+        const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+#endif
+        const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
+        const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
+                                        1.0f - 0x1p-12f, -B[3]);
+        lz.te[j] = vmax(__builtin_fmaf(lb - pl, lz.invp, tt), lz.te[j]);
+        if (wany(lz.te[j] <= tt)) due |= 1u << j;
+      }
+      lz.temin = slot_min(lz.te, ns);
+#ifdef RM_TABLE_STATIC
+      RM_TS_UNROLL
+      for (int j = 0; j < KL; ++j) {
+        if (j >= ns || !((due >> j) & 1u)) continue;
+        const int k = (int)ex[rm::EX_SLOTS + j];
+        m = vmin(m, prim_dist<kBoundedPoints>(S.entry(k), S.type(k), p, S.blend, S.omblend));
+      }
+#else
+      for (; due; due &= due - 1u) {
+        const int k = (int)ex[rm::EX_SLOTS + __builtin_ctz(due)];
+        m = vmin(m, prim_dist(S.entry(k), S.type(k), p, S.blend, S.omblend));
+      }
+#endif
+    }
+    return m;
+  };
+  float tp = t;
+  auto run = [&](auto esc, auto useT) {
+    for (int i = i0;; ++i) {
+      const float d = step(t);
+      bool e = d < 0.000001f * t;
+      dl = d;
+      tp = t;
+      t = t + d;
+      if (decltype(useT)::value) e = e | !(t <= T);
+      if (decltype(esc)::value) e = e | (d > tmax);
+      if (e | (i >= nmax)) break;
+    }
+    t = tp;
+  };
+  const bool useT = wany(!(T == __builtin_huge_valf()));
+  if (__all(S.no_escape(ro, rd, tmax))) {
+    if (useT) run(No(), Yes());
+    else run(No(), No());
+  } else {
+    if (useT) run(Yes(), Yes());
+    else run(Yes(), No());
+  }
+  if (dl < 0.000001f * t) {
+    const f3 p = add(ro, muls(rd, t));
+    int k;
+    (void)S.dist_mask(p, S.n >= 32 ? 0xffffffffu : (1u << S.n) - 1u, k);
+    asm volatile("" : "+v"(k));  // (a 32-bit index: smarch's note)
+    return THit{t, S.id(k), S.material(k), S.color(k, p), dl};
+  }
+  return THit{-1.0f, -1, 1.0f, mk(0.0f, 0.0f, 0.0f), 0.0f};
+}
+
+// RayMarch glsl:125-142 / reflectedRay glsl:144-161.  SL: the production
+// march's shape, 0 TLazy (below), 1 smarch (reference-shaped tables), 2 gmarch
+// (any plane-bounded table): the generic kernel's instance, chosen on the host
+// (rm::table_shape); a specialised table's shape is a compile-time test.
+template <bool COUNT, int KL, int SL = 0>
 __device__ RM_TS_INLINE THit tmarch(const Table& S, f3 ro, f3 rd, bool reflected, TCnt& c,
                                    const float* prep = nullptr) {
 #ifdef RM_TABLE_STATIC
   if (!COUNT && slazy_table(S)) return smarch<KL>(S, ro, rd, reflected, prep);
+  if (!COUNT && glazy_table(S)) return gmarch<KL>(S, ro, rd, reflected, prep);
 #else
-  if (!COUNT && SL) return smarch<KL>(S, ro, rd, reflected, prep);
+  if (!COUNT && SL == 1) return smarch<KL>(S, ro, rd, reflected, prep);
+  if (!COUNT && SL == 2) return gmarch<KL>(S, ro, rd, reflected, prep);
 #endif
   // ro in VGPRs (a primary ray's ro is the camera, uniform): every step's p(t)
   // then pairs for dual issue instead of taking a whole slot per component, and
@@ -899,7 +1071,7 @@ __device__ RM_TS_INLINE float tshadow(const Frame& F, const Table& S, f3 ro, f3 
 
 // bounce glsl:163-199.  Once prevObject is MATTE every later iteration leaves
 // the colour unchanged (glsl:181, 189-190): the loop stops there.
-template <bool COUNT, int KL, bool SL = false>
+template <bool COUNT, int KL, int SL = 0>
 __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3 pos, f3 normal, f3 color,
                       const THit& primary, TCnt& c) {
   float prevMat = primary.material;
@@ -948,7 +1120,7 @@ __device__ RM_TS_INLINE f3 tbounce(const Frame& F, const Table& S, f3 rayDir, f3
 }
 
 // render glsl:218-251
-template <bool COUNT, int KL, bool SL = false>
+template <bool COUNT, int KL, int SL = 0>
 __device__ RM_TS_INLINE f3 trender(const Frame& F, const Table& S, f3 ro, f3 rd, TCnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   THit h = tmarch<COUNT, KL, SL>(S, ro, rd, false, c, F.prepv);
@@ -1065,7 +1237,7 @@ __device__ __forceinline__ size_t out_index(const Frame& F, int tx, int ty, int 
 }
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
-template <bool COUNT, int KL, bool SL>
+template <bool COUNT, int KL, int SL>
 __device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x;
@@ -1096,7 +1268,7 @@ __device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds) {
 // main glsl:291-344 with 4x supersampling: one lane per (pixel, sample), the 4
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
-template <bool COUNT, int KL, bool SL>
+template <bool COUNT, int KL, int SL>
 __device__ __forceinline__ void table_sample_body(const Frame& F, float* lds) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
@@ -1139,12 +1311,12 @@ __device__ __forceinline__ void table_sample_body(const Frame& F, float* lds) {
   if (COUNT) F.sdf_counts[at] = cnt;
 }
 
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
   extern __shared__ float lds[];
   table_pixel_body<COUNT, KL, SL>(F, lds);
 }
-template <bool COUNT, int KL = rm::EX_MAX_SLOTS, bool SL = false>
+template <bool COUNT, int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
   extern __shared__ float lds[];
   table_sample_body<COUNT, KL, SL>(F, lds);
@@ -1156,13 +1328,13 @@ __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) vo
 // k_sample_frames, rm_kernels.hip).  The bodies are the kernels' above, so every
 // frame is the image of its own dispatch.  Production kernels only (a batch
 // collects no counters).
-template <int KL = rm::EX_MAX_SLOTS, bool SL = false>
+template <int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel_frames(
     FrameBatch B) {
   extern __shared__ float lds[];
   table_pixel_body<false, KL, SL>(B.f[blockIdx.z], lds);
 }
-template <int KL = rm::EX_MAX_SLOTS, bool SL = false>
+template <int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample_frames(
     FrameBatch B) {
   extern __shared__ float lds[];
@@ -1175,7 +1347,7 @@ __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) vo
 namespace rm {
 
 namespace {
-template <int KL, bool SL>
+template <int KL, int SL>
 void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
   // the table, then the lazy slots' balls (Table::sb)
   const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
@@ -1194,7 +1366,7 @@ void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
   }
 }
 
-template <int KL, bool SL>
+template <int KL, int SL>
 void launch_table_frames_kl(const rmd::FrameBatch& B, int n, hipStream_t s) {
   const rmd::Frame& F = B.f[0];
   const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
@@ -1205,19 +1377,26 @@ void launch_table_frames_kl(const rmd::FrameBatch& B, int n, hipStream_t s) {
     hipLaunchKernelGGL((rmd::k_table_pixel_frames<KL, SL>), dim3((F.width + 7) / 8, (F.rows + 7) / 8, n), dim3(64),
                        lds, s, B);
 }
+
+// The generic kernel's instance for a table: KL = TABLE_FEW_SLOTS or
+// EX_MAX_SLOTS slots (the table's lazy slots, EX_NSLOTS, fit), and the march
+// shape (rm::table_shape).
+template <class L>
+void with_instance(int nslots, int shape, L&& launch) {
+  auto sh = [&](auto kl) {
+    if (shape == 1) launch(kl, std::integral_constant<int, 1>());
+    else if (shape == 2) launch(kl, std::integral_constant<int, 2>());
+    else launch(kl, std::integral_constant<int, 0>());
+  };
+  if (nslots <= TABLE_FEW_SLOTS) sh(std::integral_constant<int, TABLE_FEW_SLOTS>());
+  else sh(std::integral_constant<int, rm::EX_MAX_SLOTS>());
+}
 }  // namespace
 
-// The frames B.f[0..n) of one table, size and AA setting in one launch: the
-// generic kernel's instance for the table (launch_table below).
-hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, bool slazy) {
+// The frames B.f[0..n) of one table, size and AA setting in one launch.
+hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, int shape) {
   if (n < 1 || n > rmd::kMaxBatch) return hipErrorInvalidValue;
-  if (nslots <= TABLE_FEW_SLOTS) {
-    if (slazy) launch_table_frames_kl<TABLE_FEW_SLOTS, true>(B, n, s);
-    else launch_table_frames_kl<TABLE_FEW_SLOTS, false>(B, n, s);
-  } else {
-    if (slazy) launch_table_frames_kl<rm::EX_MAX_SLOTS, true>(B, n, s);
-    else launch_table_frames_kl<rm::EX_MAX_SLOTS, false>(B, n, s);
-  }
+  with_instance(nslots, shape, [&](auto kl, auto sh) { launch_table_frames_kl<decltype(kl)::value, decltype(sh)::value>(B, n, s); });
   return hipGetLastError();
 }
 
@@ -1225,22 +1404,25 @@ hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, i
 // at most TABLE_FEW_SLOTS of them (the reference scene has 5) take an instance
 // holding that many: 3 fewer live expiries in the march loops, 15 -> 8 spilled
 // VGPRs at the 7-wave bound, -2.4 % per cfg3 frame.
-// slazy: the table is reference-shaped (table_slazy): the production kernels
-// take the built-in march shape (smarch); the counting kernels keep TLazy.
-hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, bool slazy) {
-  if (nslots <= TABLE_FEW_SLOTS) {
-    if (slazy) launch_table_kl<TABLE_FEW_SLOTS, true>(F, counters, s);
-    else launch_table_kl<TABLE_FEW_SLOTS, false>(F, counters, s);
-  } else {
-    if (slazy) launch_table_kl<rm::EX_MAX_SLOTS, true>(F, counters, s);
-    else launch_table_kl<rm::EX_MAX_SLOTS, false>(F, counters, s);
-  }
+// shape: the production kernels' march (rm::table_shape): 1 the built-in march
+// shape (smarch, reference-shaped tables), 2 the block shape of any
+// plane-bounded table (gmarch), 0 TLazy; the counting kernels keep TLazy.
+hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int nslots, int shape) {
+  with_instance(nslots, shape, [&](auto kl, auto sh) { launch_table_kl<decltype(kl)::value, decltype(sh)::value>(F, counters, s); });
   return hipGetLastError();
 }
 
 // smarch's conditions on a compiled table (slazy_table, device): valid exit
 // bounds; exactly one plane, the last entry, unswizzled, normal (0, n_y, 0);
 // every other entry in a lazy slot, slot j holding entry j.
+bool table_slazy(const uint32_t* words, int32_t n);
+// The production march of a compiled table: 1 smarch, 2 gmarch (valid exit
+// bounds and a plane: glazy_table, device), 0 TLazy.
+int table_shape(const uint32_t* words, int32_t n) {
+  if (table_slazy(words, n)) return 1;
+  const float* ex = reinterpret_cast<const float*>(words) + (size_t)n * TABLE_WORDS;
+  return ex[EX_VALID] != 0.0f && ex[EX_NPLANES] >= 1.0f ? 2 : 0;
+}
 bool table_slazy(const uint32_t* words, int32_t n) {
   const float* t = reinterpret_cast<const float*>(words);
   const float* ex = t + (size_t)n * TABLE_WORDS;

@@ -396,3 +396,25 @@ def test_specialisation_register_bound(rm, gpu):
         got = r.read_rgba32f()
     want = _render(rm, u, 96, 64, scene=big, counters=False)["rgba32f"]
     np.testing.assert_array_equal(got, want)
+
+
+# Tables that are not reference-shaped: several planes, the floor
+# not last, a tilted floor, more bounded entries than the lazy slots.  Their
+# production kernels march with the block shape of any plane-bounded table
+# (rm_table.hip gmarch); the counting kernels keep TLazy.
+@pytest.mark.parametrize("shape", ["planes2", "plane_mid", "tilted", "many"])
+def test_table_shapes_match_oracle(rm, oracle, gpu, shape):
+    """The counting kernel against the oracle's table mode (exact counts, <= 1 LSB),
+    the production kernel (gmarch) bit-equal to the counting image, and the
+    specialised kernels (gmarch unrolled over the table) bit-equal to the generic."""
+    from tools.probe_table_shapes import shape_table
+    sc = shape_table(shape)
+    W, H = 96, 64
+    for f, b, aa, sm in [(30, 3, True, 0), (90, 2, False, 1), (5, 5, True, 0)]:
+        u = rm.sweep_uniforms(f, 120, b, aa, sm)
+        ref = oracle.render(u, W, H, scene=sc)
+        got = _render(rm, u, W, H, scene=sc)
+        _compare(ref, got, f"{shape} f{f}")
+        prod = _render(rm, u, W, H, scene=sc, counters=False)
+        np.testing.assert_array_equal(prod["rgba32f"], got["rgba32f"])
+        _same(_render_spec(rm, u, W, H, sc, counters=False), prod)

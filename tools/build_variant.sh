@@ -37,6 +37,7 @@ if [ -f "$src/$pkg/csrc/rm_jit.hip" ]; then  # per-table hiprtc kernels: embed t
   c=$src/$pkg/csrc
   python3 "$src/$pkg/tools/embed_sources.py" "$b/rm_jit_src.inc" rm_table.hip=$c/rm_table.hip \
     rm_internal.hpp=$c/rm_internal.hpp rm_scene.hpp=$c/rm_scene.hpp rm_fastmath.hpp=$c/rm_fastmath.hpp \
+    $( [ -f "$c/rm_shard.hpp" ] && echo rm_shard.hpp=$c/rm_shard.hpp ) \
     ../../include/rm_api.h=$src/include/rm_api.h
   /opt/rocm/bin/hipcc $flags -I"$b" -c "$c/rm_jit.hip" -o "$b/rm_jit.o" &
 fi
