@@ -357,12 +357,7 @@ void prep_host(const float cam[3], float blend, float omblend, float out[16]) {
   for (int k = 0; k < 5; ++k) {
     // the gaps of scene_lazy's re-test at the camera with U = d0, in its float
     // operations: g = (lb - d0) - slack, plane gap lb - pl
-    float lb = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
-    if (k == 3) {  // the torus's own bound (rm_scene.hpp torus_lb), IEEE sqrt within its margins
-      const float r = std::sqrt(cx2 + ay2);
-      const float a = std::fmax(std::fma(r, -0x1p-12f, std::fabs(r - 2.5f)), 0.0f);
-      lb = std::fma(std::sqrt(std::fma(a, a, tz * tz)), CULL_REL_LO, -(CULL_ABS + 0.5f));
-    }
+    const float lb = std::fma(std::sqrt(x[k]), CULL_REL_LO, -(CULL_ABS + R[k]));
     const float g = lb - d - sl;
     out[PREP_G + k] = g > 0.0f ? g : -INFINITY;
     out[PREP_H + k] = g > 0.0f ? lb - pl : -INFINITY;

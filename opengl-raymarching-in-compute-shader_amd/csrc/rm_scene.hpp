@@ -349,23 +349,6 @@ __device__ __forceinline__ float scene_cull(f3 p, float blend, float omblend, in
   return m;
 }
 
-// A lower bound of the torus's distance (glsl:93-96,119), the torus's own
-// shape instead of its ball (round 5).  With q = (p - c).xzy, rho = |(q.x, q.z)|
-// = |(cx, ay)| and q.y = tz (the float offsets the exact evaluation uses), the
-// distance is D = |(rho - 2.5, tz)| - 0.5 >= |p - c| - 3, the ball's bound, and
-// far tighter beside the ring's axis and off its plane, where most re-tests of
-// the torus happened (cfg3: 10 of 21 per wave, 7.5 exact evaluations).  Raw
-// v_sqrt (1.5 ulp) and float sums err by a few ulp; a = ||rho| - 2.5| is lowered
-// by rho 2^-12 (covering rho's error and the subtraction's rounding, which is
-// below u max(rho, 2.5), where 2.5 2^-12 of the outer factor takes over), the
-// outer sqrt by the relative 2^-12 and the absolute CULL_ABS of every ball bound.
-__device__ __forceinline__ float torus_lb(float cx2ay2, float tz) {
-  const float r = __builtin_amdgcn_sqrtf(cx2ay2);
-  const float a = fmaxf(__builtin_fmaf(r, -0x1p-12f, fabsf(r - 2.5f)), 0.0f);
-  const float B = __builtin_fmaf(a, a, tz * tz);
-  return __builtin_fmaf(__builtin_amdgcn_sqrtf(B), CULL_REL_LO, -(CULL_ABS + 0.5f));
-}
-
 // ---- GetNormal's samples with shared culling (glsl:278-288) --------------------------
 // sdf at pos and at pos + 0.001 e_x/e_y/e_z.  The four points lie within
 // e = 0.001 + 2^-22 (|pos|_1 + 1) of pos (the float adds round), so by the
@@ -585,11 +568,11 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       idp = (v <= m) ? k : idp;
       m = vmin(m, v);
     };
-    // re-test k against its lower bound lb; returns true when k must be
-    // evaluated exactly at this step
-    auto retest_lb = [&](float lb, float& te, int k) -> bool {
+    // re-test k; returns true when k must be evaluated exactly at this step
+    auto retest = [&](float x, float R, float& te, int k) -> bool {
       RM_STAT(1);
       RM_STAT(16 + k);
+      const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
       // The new expiry is the later of the old one and the plane budget's end;
       // both are valid, so their max is.  A gap lb - pl <= 0 ends the budget at
       // or before t, leaving an expired lane with te <= t: evaluated now and
@@ -604,10 +587,6 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       // extra exact evaluation, never a wrong skip.  One compare instead of two
       // (`expired & !(g > 0)`, round 3).
       return te <= t;
-    };
-    // the ball bound |p - c| - R
-    auto retest = [&](float x, float R, float& te, int k) -> bool {
-      return retest_lb(__builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R)), te, k);
     };
     const f3 p = mk(ro.x + rd.x * t, py, ro.z + rd.z * t);
     const Offs o = offsets(p);
@@ -638,9 +617,9 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
         take(sd_blend(o, xs, blend, omblend), 4);
       }
     }
-    if (__any(t >= lc.te[3])) {  // torus, glsl:119 (its own bound, torus_lb)
+    if (__any(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      if (retest_lb(torus_lb(o.cx2 + o.ay2, tz), lc.te[3], 3)) {
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
         RM_STAT(13);
         take(sd_torus(o, tz), 5);
       }
