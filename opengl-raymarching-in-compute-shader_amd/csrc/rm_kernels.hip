@@ -421,9 +421,9 @@ __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
 // 39x39 tiles; its W/wg truncation band (main.cpp:123) is not reproduced.
 constexpr int kTileW = 8, kTileH = 8;
 template <bool COUNT>
-__device__ __forceinline__ void pixel_body(const Frame& F) {
+__device__ __forceinline__ void pixel_body(const Frame& F, int rowslot) {
   const int lane = threadIdx.x & 63;
-  const int by = tile_row(blockIdx.y, F.grid_y);
+  const int by = tile_row(rowslot, F.grid_y);
   const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kTileW * 4));
   const int px = bx * kTileW + (lane & 7);
   const int lrow = by * kTileH + (lane >> 3);
@@ -464,10 +464,10 @@ __device__ __forceinline__ void pixel_body(const Frame& F) {
 // lane shuffles before the /4 (glsl:315-335).
 constexpr int kSampleTileW = 4, kSampleTileH = 4;
 template <bool COUNT>
-__device__ __forceinline__ void sample_body(const Frame& F) {
+__device__ __forceinline__ void sample_body(const Frame& F, int rowslot) {
   const int lane = threadIdx.x & 63;
   const int s = lane & 3, q = lane >> 2;
-  const int by = tile_row(blockIdx.y, F.grid_y);
+  const int by = tile_row(rowslot, F.grid_y);
   const int bx = tile_col(blockIdx.x, F.grid_x, 128 / (kSampleTileW * 4));
   const int px = bx * kSampleTileW + q % kSampleTileW;
   const int lrow = by * kSampleTileH + q / kSampleTileW;
@@ -538,7 +538,7 @@ __device__ __forceinline__ void sample_body(const Frame& F) {
 #ifndef RM_KERNELS_AA_ONLY
 template <bool COUNT>
 __global__ __launch_bounds__(64, 8) void k_pixel(Frame F) {
-  pixel_body<COUNT>(F);
+  pixel_body<COUNT>(F, blockIdx.y);
 }
 #endif
 #ifndef RM_KERNELS_PIXEL_ONLY
@@ -548,22 +548,35 @@ __global__ __launch_bounds__(64, 8) void k_pixel(Frame F) {
 // profiles/r03_compiler_ab.txt); k_pixel keeps it (1-2 % faster with it, cfg2).
 template <bool COUNT>
 __global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
-  sample_body<COUNT>(F);
+  sample_body<COUNT>(F, blockIdx.y);
 }
 #endif
 
-// Frame batches (rm_dispatch_frames): grid.z = the frame.  The hardware
-// dispatches workgroups in x, y, z order, so the slow middle rows of frame z + 1
-// (inside-out order, tile_row) start while frame z's longest waves still run:
-// one tail per batch instead of one per frame.  Production builds only.
+// Frame batches (rm_dispatch_frames): n frames in one grid of gridDim.y x n tile
+// rows.  The hardware dispatches workgroups in x, y, z order; (y, z) is read
+// row-major over the frames: dispatch slot L = z gridDim.y + y renders tile-row
+// slot L / n (inside-out order, tile_row) of frame L % n, so the slowest rows of
+// every frame of the batch start first and the launch ends on the cheap rows of
+// all its frames (round 5; frame-major order ended each launch on its last
+// frame's cheap rows but started every frame's slow rows only after the previous
+// frame's whole grid).  Production builds only.
+__device__ __forceinline__ void batch_slot(int& frame, int& rowslot) {
+  const int L = blockIdx.z * gridDim.y + blockIdx.y, n = gridDim.z;
+  rowslot = L / n;
+  frame = L - rowslot * n;
+}
 #ifndef RM_KERNELS_AA_ONLY
 __global__ __launch_bounds__(64, 8) void k_pixel_frames(FrameBatch B) {
-  pixel_body<false>(B.f[blockIdx.z]);
+  int f, r;
+  batch_slot(f, r);
+  pixel_body<false>(B.f[f], r);
 }
 #endif
 #ifndef RM_KERNELS_PIXEL_ONLY
 __global__ __launch_bounds__(64, 8) void k_sample_frames(FrameBatch B) {
-  sample_body<false>(B.f[blockIdx.z]);
+  int f, r;
+  batch_slot(f, r);
+  sample_body<false>(B.f[f], r);
 }
 #endif
 

@@ -81,15 +81,26 @@ def test_oracle_rejects_bad_tables(rm, oracle):
                               None, None, 1) == -1
 
 
+_CO_CACHE = {}
+
+
 def _code_object(rm, scene, arch=b"gfx950"):
+    """rm_jit_code_object: every call compiles, so one call with room to spare (a
+    second, larger one only if the object outgrows it), cached per table."""
     tbl = (rm.rm_primitive * len(scene))(*scene)
+    key = (bytes(tbl), arch)
+    if key in _CO_CACHE:
+        return _CO_CACHE[key]
     size = C.c_size_t(0)
-    rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, None, 0, C.byref(size))
-    if rc != 0:
-        return rc, b""
-    buf = C.create_string_buffer(size.value)
-    rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, buf, size.value, C.byref(size))
-    return rc, buf.raw
+    cap = 4 << 20
+    buf = C.create_string_buffer(cap)
+    rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, buf, cap, C.byref(size))
+    if rc == rm.RM_ERR_INVALID and size.value > cap:
+        buf = C.create_string_buffer(size.value)
+        rc = rm.lib().rm_jit_code_object(tbl, len(scene), arch, buf, size.value, C.byref(size))
+    out = (rc, buf.raw[:size.value] if rc == 0 else b"")
+    _CO_CACHE[key] = out
+    return out
 
 
 def _kernel_private_sizes(co):
