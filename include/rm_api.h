@@ -298,7 +298,9 @@ int rm_scene_specialize(rm_ctx *ctx, int enable);
 /* The register bound of the specialised table kernels in use: *waves = the
  * waves per SIMD they were compiled for (8, 7 or 6: the most at which they need
  * no scratch), or 0 when the generic table kernel (or the built-in scene)
- * renders; a table that spills at 6 waves is not specialised. */
+ * renders; a table that spills at 6 waves is not specialised, and neither is
+ * one of more than 12 entries (not compiled at all: past a dozen entries the
+ * compile takes minutes and fits no bound). */
 int rm_scene_kernel_waves(const rm_ctx *ctx, int32_t *waves);
 /* Diagnostics (API version 5): the table as rm_set_scene compiles it on the host
  * for the device (no device needed): the n entries' words, then the exit header

@@ -19,9 +19,10 @@
 // 1), whose descriptors give each production kernel's VGPR allocation (a kernel
 // allocating at most 512 / w registers runs at w waves with no scratch), and
 // only for a table needing more than 80 registers one more, bounded to 6 waves,
-// kept if it needs no scratch; one that spills even there (a 30-entry table
-// spills 100+ VGPRs at 4 waves) is not specialised and renders with the generic
-// (LDS-staged) kernel, whose registers do not grow with the table.  The
+// kept if it needs no scratch; one that spills even there is not specialised
+// and renders with the generic (LDS-staged) kernel, whose registers do not grow
+// with the table, and so does a table of more than kJitMaxEntries entries,
+// without a compile (below).  The
 // reference scene compiles once.  RM_JIT_LOG=1 prints one line
 // per hiprtc compile (stderr).
 //
@@ -212,6 +213,13 @@ long production_scratch(const std::vector<char>& c, const std::vector<std::strin
 }
 
 constexpr long kFewSpillBytes = 32;  // 8 spilled VGPRs per lane
+// Larger tables are not compiled: the unrolled kernels' registers grow with the
+// table, and past a dozen entries hiprtc spends minutes producing spill code that
+// fits no bound (the reference scene's objects repeated, on the build host's
+// CPU: 12 entries 26 s, one compile that fits 8 waves; 16 entries 261 s for the
+// 8-wave compile alone, 3.7 MB of code, and 786 s for the ladder, which ends
+// on the generic kernel).  They render with the generic kernel at once.
+constexpr int32_t kJitMaxEntries = 12;
 
 // The table kernels at their register bound (above): *waves is the waves per
 // SIMD they run at, or 0 (code left empty) when no bound fits.
@@ -219,6 +227,7 @@ int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::
                 std::vector<std::string>& lowered, std::string& err, int* waves) {
   if (waves) *waves = 0;
   code.clear();
+  if (n > kJitMaxEntries) return RM_OK;
   std::vector<char> c;
   std::vector<std::string> l;
   if (const char* fw = std::getenv("RM_JIT_FORCE_WAVES"); fw && *fw) {

@@ -142,6 +142,18 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll 1
       for (;;) {
         if (live) {
+#ifdef RM_STEP_TOPMX
+          for (int i = ib;; ++i) {
+            if (decltype(usemx)::value && !(t <= mx)) break;
+            const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+            bool ex = d < 0.000001f * t;
+            dl = d;
+            if (decltype(esc)::value) ex = ex | (d > tmax);
+            if (ex | (i >= iend)) break;
+            t = t + d;
+          }
+          if (decltype(usemx)::value) dl = (t <= mx) ? dl : QNAN;
+#else
           float tp = t;
           for (int i = ib;; ++i) {
 #ifdef RM_WAVE_STATS
@@ -157,6 +169,7 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
             if (ex | (i >= iend)) break;
           }
           t = tp;
+#endif
         }
         if (iend >= nmax) break;
         {

@@ -380,8 +380,9 @@ def test_specialisation_register_bound(rm, gpu):
     """rm_jit.hip compiles a table for the most waves per SIMD (8, 7, 6) at which
     its production kernels need no scratch (one fixed 8-wave bound
     spilled for the reference scene and spilled hundreds of VGPRs for large
-    tables).  The reference scene specialises; a 30-entry table fits no such
-    bound and renders with the generic kernel, with the same image."""
+    tables).  The reference scene specialises; a 30-entry table is not compiled
+    (more than 12 entries, rm_jit.hip kJitMaxEntries) and renders with the generic
+    kernel, with the same image."""
     u = rm.sweep_uniforms(60, 120, 3, True, 0)
     with rm.Renderer(96, 64, outputs=OUT) as r:
         assert r.scene_kernel_waves() == 0  # built-in scene

@@ -181,6 +181,31 @@ def test_table_compiles_once(rm, tmp_path):
     assert len(prod) == 4 and all(v <= 64 for v in prod.values()), vg  # 8 waves per SIMD
 
 
+def test_large_tables_are_not_compiled(rm):
+    """A table of more than 12 entries is not specialised and costs no hiprtc
+    compile (a 16-entry table took 786 s of compiles to end on the generic kernel,
+    rm_jit.hip kJitMaxEntries): *size = 0 at once, no compile logged."""
+    import subprocess
+    import sys
+    prog = (
+        "import ctypes as C, sys\n"
+        f"sys.path.insert(0, {os.path.dirname(rm.__file__)!r}.rsplit('/', 1)[0])\n"
+        "import rmarch as rm\n"
+        "sc = rm.default_scene()\n"
+        "sc = sc[:-1] * 3 + sc[-1:]\n"
+        "assert len(sc) == 16\n"
+        "for n in (13, 16):\n"
+        "    t = sc[:n - 1] + sc[-1:]\n"
+        "    tbl = (rm.rm_primitive * n)(*t)\n"
+        "    size = C.c_size_t(1)\n"
+        "    assert rm.lib().rm_jit_code_object(tbl, n, b'gfx950', None, 0, C.byref(size)) == 0\n"
+        "    assert size.value == 0\n")
+    out = subprocess.run([sys.executable, "-c", prog], env=dict(os.environ, RM_JIT_LOG="1"),
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "hiprtc compile" not in out.stderr, out.stderr
+
+
 def _kernel_vgprs(co):
     """VGPR allocation per lane of every kernel (compute_pgm_rsrc1 bits 5:0 of its
     descriptor at offset 48: allocation / 8 - 1 on gfx950)."""
