@@ -353,6 +353,7 @@ void prep_host(const float cam[3], float blend, float omblend, float out[16]) {
   out[PREP_SLACK] = sl;
   out[PREP_B1] = (rc + SH_RALL + sl + 0.0f) * HI;
   out[PREP_B2] = ((py + 5.5f) - sl - 0.0f * HI) - 0x1p-19f * (std::fabs(py) + 5.5f + 0.0f + sl);
+  out[PREP_B3] = ((SH_YTOP - py) + sl + 0.0f * HI) + 0x1p-19f * (std::fabs(py) + SH_YTOP + 0.0f + sl);
   const float pl = (py + 5.5f) + sl;
   for (int k = 0; k < 5; ++k) {
     // the gaps of scene_lazy's re-test at the camera with U = d0, in its float

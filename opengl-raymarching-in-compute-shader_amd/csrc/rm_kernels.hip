@@ -79,7 +79,14 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     } else {
       lin_exit_b(ro, s0, 0.0f, b1, b2);
     }
-    return lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2);
+    float b3 = __builtin_huge_valf();
+#ifdef RM_EXIT_PROJ
+    b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, UNIT ? 1.0f : __builtin_amdgcn_rcpf(rdl), s0, 0.0f));
+#endif
+#ifdef RM_EXIT_YSLAB
+    b3 = prep ? F.prepv[PREP_B3] : lin_exit_b3(ro.y, s0, 0.0f);
+#endif
+    return lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2, b3);
   };
   // lin_exit's object bound T1 for the step-cap check, re-formed there from the
   // ray (rare) rather than kept live through the loop
@@ -142,7 +149,27 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll 1
       for (;;) {
         if (live) {
-#ifdef RM_STEP_TOPMX
+#if defined(RM_STEP_MX2)
+          // two steps per iteration, the proven-miss test before the first only
+          // (a lane past mx is a proven miss: marching on cannot hit, it only
+          // costs the step)
+          for (int i = ib;; i += 2) {
+            if (decltype(usemx)::value && !(t <= mx)) break;
+            float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+            bool ex = d < 0.000001f * t;
+            dl = d;
+            if (decltype(esc)::value) ex = ex | (d > tmax);
+            if (ex | (i >= iend)) break;
+            t = t + d;
+            d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
+            ex = d < 0.000001f * t;
+            dl = d;
+            if (decltype(esc)::value) ex = ex | (d > tmax);
+            if (ex | (i + 1 >= iend)) break;
+            t = t + d;
+          }
+          if (decltype(usemx)::value) dl = (t <= mx) ? dl : QNAN;
+#elif defined(RM_STEP_TOPMX)
           for (int i = ib;; ++i) {
             if (decltype(usemx)::value && !(t <= mx)) break;
             const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);

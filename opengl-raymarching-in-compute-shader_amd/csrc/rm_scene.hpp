@@ -478,7 +478,8 @@ enum PrepSlot : int {
   PREP_H = 8,       // 5 plane gaps LB_k - (plane(camera) + slack), or -inf when g_k <= 0
   PREP_B1 = 13,     // lin_exit_b(camera, slack, 0): the miss exit's ro-dependent terms
   PREP_B2 = 14,
-  PREP_COUNT = 15
+  PREP_B3 = 15,     // lin_exit_b3(camera, slack, 0): the object slab's intercept
+  PREP_COUNT = 16
 };
 // Per-ray constants shared by the lazy culler and the linear exits: |rd| from
 // one v_sqrt (within 1.5 ulp) and the slack line s0 + s1 t, rounded up with
@@ -679,24 +680,73 @@ __device__ __forceinline__ void lin_exit_b(f3 ro, float s0, float hmin, float& b
   b1 = (rc + SH_RALL + s0 + hmin) * HI;
   b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
 }
-__device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float s1, float b1, float b2) {
+constexpr float SH_YTOP = 3.001f;  // >= the top of every bounded primitive (below)
+#if defined(RM_EXIT_YSLAB) || defined(RM_EXIT_PROJ)
+// Two more lower bounds of the five objects (round 5), each linear in t like the
+// ball's, so either one holding from t_j on proves the objects term as well:
+//   * the slab below SH_YTOP, which holds every bounded primitive (each reaches
+//     y = 3 and no higher: the spheres, the blend's sphere over its box, the
+//     torus ring in its vertical plane, the capsule's end (-3, 2, -28) + 1):
+//     objects >= p.y - SH_YTOP - err, so with the plane's slope a2
+//       a2 t - b3 > 0,  b3 = SH_YTOP + s0 + hmin - ro.y   (rounded up),
+//     T3 = b3 / a2: an upward ray is past every object once above the slab;
+//   * the ball seen along the ray: |p(t) - C| >= |rd| t + u with
+//     u = rd.(ro - C) / |rd| (|p - C|^2 = (|rd| t + u)^2 + |ro - C|^2 - u^2),
+//     so b1 may take -u (rounded down) for |ro - C|: a ray leaving the ball is
+//     past it at once, where the triangle inequality waits for |rd| t > |ro - C|
+//     + R_ALL.  (The step-cap exit keeps the plain b1.)
+// A blend of box and sphere (weights in [0, 1] summing to 1) is above the lower
+// of the two, so both bounds cover it as the ball does.
+__device__ __forceinline__ float lin_exit_b3(float roy, float s0, float hmin) {
+  return ((SH_YTOP - roy) + s0 + hmin * (1.0f + 0x1p-12f)) +
+         0x1p-19f * (fabsf(roy) + SH_YTOP + hmin + s0);
+}
+// b1 from the projection, rounded up: every rounding of e, the dot product and
+// the 1 / |rd| scaling is within 2^-17 |ro - C|_1 (|u| <= |ro - C|), and the
+// sum's within 2^-17 of its terms.  invl: 1 / |rd| within 2^-20 (1 for unit rays).
+__device__ __forceinline__ float lin_exit_b1p(f3 ro, f3 rd, float invl, float s0, float hmin) {
+  const float ex = ro.x - SH_CX, ey = ro.y - SH_CY, ez = ro.z - SH_CZ;
+  const float u = ((rd.x * ex + rd.y * ey) + rd.z * ez) * invl;
+  const float e1 = (fabsf(ex) + fabsf(ey)) + fabsf(ez);
+  const float k = (SH_RALL + s0) + hmin;
+  return (k - u) + 0x1p-17f * (e1 + k);
+}
+#endif
+__device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float s1, float b1, float b2,
+                                            float b3 = __builtin_huge_valf()) {
   const float LO = 1.0f - 0x1p-12f;
   // absolute 2^-20 terms: the rounding of a difference is relative to its
   // operands, not to a small (cancelled) result
   const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
   const float a2 = (rdy - s1 - c) * LO - 0x1p-20f * (fabsf(rdy) + s1 + c);
   const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
+  const float INF = __builtin_huge_valf();
+#if defined(RM_EXIT_YSLAB) || defined(RM_EXIT_PROJ)
+  // b1 may be negative (the projection): T1 rounded up either way
+  const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * (b1 >= 0.0f ? UP : DN);
+  const float r2 = __builtin_amdgcn_rcpf(a2);
+  const float T2 = -(b2 * r2 * (b2 >= 0.0f ? DN : UP));
+  const float T3 = b3 * r2 * (b3 >= 0.0f ? UP : DN);  // +inf for b3 = +inf
+  const float Tobj = a1 > 0.0f ? __builtin_fminf(T1, T3) : T3;
+  return a2 > 0.0f ? __builtin_fmaxf(Tobj, T2) : INF;
+#else
   const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * UP;
   const float T2 = -(b2 * __builtin_amdgcn_rcpf(a2) * (b2 >= 0.0f ? DN : UP));
-  const float INF = __builtin_huge_valf();
   return (a1 > 0.0f && a2 > 0.0f) ? __builtin_fmaxf(T1, T2) : INF;
+#endif
 }
 constexpr float MISS_C = 0.000001f * (1.0f + 0x1p-9f);
 __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd, float rdl) {
   const float s0 = ray_s0(ro);
-  float b1, b2;
+  float b1, b2, b3 = __builtin_huge_valf();
   lin_exit_b(ro, s0, hmin, b1, b2);
-  return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2);
+#ifdef RM_EXIT_PROJ
+  b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, __builtin_amdgcn_rcpf(rdl), s0, hmin));
+#endif
+#ifdef RM_EXIT_YSLAB
+  b3 = lin_exit_b3(ro.y, s0, hmin);
+#endif
+  return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2, b3);
 }
 // c = Frame::shc, (1 + 2^-9) / k (1 + 2^-12) (0 for k = +inf): the host forms it
 // with the same float operations once per frame (rm_api.hip make_frame), where
