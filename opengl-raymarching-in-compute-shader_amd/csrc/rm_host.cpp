@@ -479,6 +479,10 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
   std::memset(h, 0, sizeof h);
   std::vector<double> cx, cy, cz, rr;
   std::vector<int32_t> ball_of;  // entry of each ball
+  // the bounded entries' box: each entry's value is at least its distance to
+  // the solid it bounds (exact sdfs; a blend is above the lower of its box and
+  // sphere), so at least the distance to the solid's box, per axis
+  double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
   double S = 0.0, N = 1.0, lip = 1.0;
   int np = 0;
   bool ok = true;
@@ -497,15 +501,35 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
       o[2] = p.swizzle == RM_SWIZZLE_XZY ? y : z;
     };
     double m[3] = {0.0, 0.0, 0.0}, R = 0.0;
+    double qlo[3] = {0.0, 0.0, 0.0}, qhi[3] = {0.0, 0.0, 0.0};  // the solid's box, q-space
+    auto sym = [&](double hx, double hy, double hz) {
+      const double hh[3] = {hx, hy, hz};
+      for (int j = 0; j < 3; ++j) qlo[j] = -hh[j], qhi[j] = hh[j];
+    };
     switch (p.type) {
-      case RM_PRIM_SPHERE: R = a[0]; break;
+      case RM_PRIM_SPHERE:
+        R = a[0];
+        sym(std::max(a[0], 0.0), std::max(a[0], 0.0), std::max(a[0], 0.0));
+        break;
       case RM_PRIM_BOX:
       case RM_PRIM_BLEND:
         if (a[0] < 0.0 || a[1] < 0.0 || a[2] < 0.0) ok = false;
         R = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-        if (p.type == RM_PRIM_BLEND) R = std::max(R, a[3]);
+        if (p.type == RM_PRIM_BLEND) {
+          R = std::max(R, a[3]);
+          const double r = std::max(a[3], 0.0);
+          sym(std::max(a[0], r), std::max(a[1], r), std::max(a[2], r));
+        } else {
+          sym(a[0], a[1], a[2]);
+        }
         break;
-      case RM_PRIM_TORUS: R = std::fabs(a[0]) + a[1]; break;
+      case RM_PRIM_TORUS: {
+        // the ring in the q.xz plane: |q.xz| <= |R| + r, |q.y| <= r
+        R = std::fabs(a[0]) + a[1];
+        const double r = std::max(a[1], 0.0), w = std::fabs(a[0]) + r;
+        sym(w, r, w);
+        break;
+      }
       case RM_PRIM_CAPSULE: {
         const double bx = a[3] - a[0], by = a[4] - a[1], bz = a[5] - a[2];
         const double bl = std::sqrt(bx * bx + by * by + bz * bz);
@@ -514,6 +538,8 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
         if (!((fbx * fbx + fby * fby) + fbz * fbz > 0.0f)) ok = false;
         world(a[0] + bx / 2, a[1] + by / 2, a[2] + bz / 2, m);
         R = bl / 2 + a[6];
+        const double r = std::max(a[6], 0.0);
+        for (int j = 0; j < 3; ++j) qlo[j] = std::min(a[j], a[3 + j]) - r, qhi[j] = std::max(a[j], a[3 + j]) + r;
         break;
       }
       default: {  // plane
@@ -535,6 +561,15 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
     cx.push_back(p.center[0] + m[0]);
     cy.push_back(p.center[1] + m[1]);
     cz.push_back(p.center[2] + m[2]);
+    {
+      double wl[3], wh[3];  // the swizzle permutes axes: the box maps to a box
+      world(qlo[0], qlo[1], qlo[2], wl);
+      world(qhi[0], qhi[1], qhi[2], wh);
+      for (int j = 0; j < 3; ++j) {
+        blo[j] = std::min(blo[j], (double)p.center[j] + wl[j]);
+        bhi[j] = std::max(bhi[j], (double)p.center[j] + wh[j]);
+      }
+    }
     rr.push_back(R);
     ball_of.push_back(k);
   }
@@ -558,6 +593,10 @@ static void exit_bounds(const rm_primitive* prims, int32_t n, uint32_t* out) {
   h[EX_S] = (float)((S + 1.0) * (1.0 + 0x1p-20));
   h[EX_NPLANES] = (float)np;
   h[EX_LIP] = (float)(lip * (1.0 + 0x1p-20));
+  for (int j = 0; j < 3; ++j) {  // rounded outward (no bounded entry: an empty box)
+    h[EX_BOX + j] = cx.empty() ? 0.0f : (float)(blo[j] - 0x1p-20 * (1.0 + std::fabs(blo[j])));
+    h[EX_BOX + 3 + j] = cx.empty() ? 0.0f : (float)(bhi[j] + 0x1p-20 * (1.0 + std::fabs(bhi[j])));
+  }
   uint32_t eval_mask = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
   int ns = 0;
   for (size_t j = 0; ok && j < ball_of.size() && ns < EX_MAX_SLOTS; ++j) {

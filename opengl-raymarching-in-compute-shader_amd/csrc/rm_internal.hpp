@@ -36,8 +36,9 @@ enum TableWord : int {
 // After the n entries: EXIT_WORDS words of per-table bounds for the provable
 // early exits of the table kernels (rm_table.hip): every non-plane entry lies in
 // the ball (EX_C, EX_R); planes are linear along a ray; EX_SIGMA, EX_S scale the
-// float-error slack.  EX_VALID = 0 disables the exits (unbounded or degenerate
-// entries, more than EX_MAX_PLANES planes).
+// float-error slack; every non-plane entry also lies in the box EX_BOX (round
+// 5: the slab exits of table_exit_T).  EX_VALID = 0 disables the exits
+// (unbounded or degenerate entries, more than EX_MAX_PLANES planes).
 // The same header lists the entries the march tracks lazily (EX_SLOTS, at most
 // EX_MAX_SLOTS bounded entries, in table order), the bitmask of the entries
 // evaluated at every step (EX_EVAL_MASK, bit k = entry k: planes and untracked
@@ -52,7 +53,8 @@ enum ExitWord : int {
   EX_VALID = 0, EX_CX = 1, EX_CY = 2, EX_CZ = 3, EX_R = 4, EX_SIGMA = 5, EX_S = 6,
   EX_NPLANES = 7, EX_PLANES = 8,  // per plane: world normal n' (3), offset: value ~ dot(p, n') + off
   EX_LIP = EX_PLANES + 4 * EX_MAX_PLANES, EX_NSLOTS, EX_EVAL_MASK, EX_PLANE_MASK, EX_SLOTS,
-  EX_END = EX_SLOTS + EX_MAX_SLOTS,
+  EX_BOX = EX_SLOTS + EX_MAX_SLOTS,  // the bounded entries' box: lo (3), hi (3), rounded outward
+  EX_END = EX_BOX + 6,
 };
 constexpr int EXIT_WORDS = EX_END;
 // Step 0 of a table's primary rays, formed on the host per frame (rm_api.hip

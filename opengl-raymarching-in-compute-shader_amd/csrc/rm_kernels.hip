@@ -49,7 +49,9 @@ __device__ __forceinline__ f3 opaque(f3 v) { return mk(opaque(v.x), opaque(v.y),
 // needs |rd| from below or above, with the bounds' own 2^-12 / 2^-16 margins
 // (it stood for a v_sqrt within 1.5 ulp), so |rd|, its reciprocal and the
 // slack slope become constants and the miss exit's object bound is uniform.
-template <bool COUNT, bool UNIT = false>
+// PPROJ: primary rays take the projection bound of the miss exit too (k_pixel;
+// see miss_T).
+template <bool COUNT, bool UNIT = false, bool PPROJ = false>
 __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3& col, Cnt& c,
                        float& dlast) {
   float t = 0.0f, dl = 0.0f;
@@ -79,13 +81,14 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
     } else {
       lin_exit_b(ro, s0, 0.0f, b1, b2);
     }
-    float b3 = __builtin_huge_valf();
-#ifdef RM_EXIT_PROJ
-    b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, UNIT ? 1.0f : __builtin_amdgcn_rcpf(rdl), s0, 0.0f));
-#endif
-#ifdef RM_EXIT_YSLAB
-    b3 = prep ? F.prepv[PREP_B3] : lin_exit_b3(ro.y, s0, 0.0f);
-#endif
+    // the objects' ball seen along the ray: reflected rays, and the primary rays
+    // of frames without supersampling.  A primary ray from the camera mostly heads
+    // into the scene, where the projection is close to |ro - C|: in 4x-supersampled
+    // frames the bound costs more than it saves (cfg3 +0.4 %), in k_pixel's frames
+    // it saves (cfg2 -3.5 %, profiles/r05_ab_exits2.txt)
+    if (!prep || PPROJ)
+      b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, UNIT ? 1.0f : __builtin_amdgcn_rcpf(rdl), s0, 0.0f));
+    const float b3 = prep ? F.prepv[PREP_B3] : lin_exit_b3(ro.y, s0, 0.0f);
     return lin_exit_T(MISS_C, rdl, rd.y, s1, b1, b2, b3);
   };
   // lin_exit's object bound T1 for the step-cap check, re-formed there from the
@@ -149,38 +152,6 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
 #pragma unroll 1
       for (;;) {
         if (live) {
-#if defined(RM_STEP_MX2)
-          // two steps per iteration, the proven-miss test before the first only
-          // (a lane past mx is a proven miss: marching on cannot hit, it only
-          // costs the step)
-          for (int i = ib;; i += 2) {
-            if (decltype(usemx)::value && !(t <= mx)) break;
-            float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-            bool ex = d < 0.000001f * t;
-            dl = d;
-            if (decltype(esc)::value) ex = ex | (d > tmax);
-            if (ex | (i >= iend)) break;
-            t = t + d;
-            d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-            ex = d < 0.000001f * t;
-            dl = d;
-            if (decltype(esc)::value) ex = ex | (d > tmax);
-            if (ex | (i + 1 >= iend)) break;
-            t = t + d;
-          }
-          if (decltype(usemx)::value) dl = (t <= mx) ? dl : QNAN;
-#elif defined(RM_STEP_TOPMX)
-          for (int i = ib;; ++i) {
-            if (decltype(usemx)::value && !(t <= mx)) break;
-            const float d = scene_lazy(ro, rd, t, lc, F.blend, F.omblend);
-            bool ex = d < 0.000001f * t;
-            dl = d;
-            if (decltype(esc)::value) ex = ex | (d > tmax);
-            if (ex | (i >= iend)) break;
-            t = t + d;
-          }
-          if (decltype(usemx)::value) dl = (t <= mx) ? dl : QNAN;
-#else
           float tp = t;
           for (int i = ib;; ++i) {
 #ifdef RM_WAVE_STATS
@@ -196,7 +167,6 @@ __device__ float march(const Frame& F, f3 ro, f3 rd, bool reflected, int& id, f3
             if (ex | (i >= iend)) break;
           }
           t = tp;
-#endif
         }
         if (iend >= nmax) break;
         {
@@ -404,15 +374,15 @@ __device__ f3 bounce(const Frame& F, f3 rayDir, f3 pos, f3 normal, f3 color, f3 
 }
 
 // render glsl:218-251
-template <bool COUNT>
+template <bool COUNT, bool PPROJ = false>
 __device__ __forceinline__ f3 render(const Frame& F, f3 ro, f3 rd, Cnt& c) {
   f3 color = subs(mk(0.30f, 0.36f, 0.60f), rd.y * 0.2f);
   int id;
   f3 hcol;
   float dl;
   // (F.unit_rd is uniform: one march or the other for the whole wave)
-  float th = F.unit_rd ? march<COUNT, true>(F, ro, rd, false, id, hcol, c, dl)
-                       : march<COUNT, false>(F, ro, rd, false, id, hcol, c, dl);
+  float th = F.unit_rd ? march<COUNT, true, PPROJ>(F, ro, rd, false, id, hcol, c, dl)
+                       : march<COUNT, false, PPROJ>(F, ro, rd, false, id, hcol, c, dl);
 #ifdef RM_DBL_MARCH
   if (!COUNT) {
     int id2; f3 hc2; float dl2;
@@ -476,7 +446,7 @@ __device__ __forceinline__ void pixel_body(const Frame& F, int rowslot) {
     f3 ro, rd;
     cast_ray(F, lane_uv(F, 0, px, -1), lane_uv(F, 1, py, -1), ro, rd);
     if (COUNT) c.rays++;
-    f3 col = render<COUNT>(F, ro, rd, c);
+    f3 col = render<COUNT, true>(F, ro, rd, c);
     o0 = col.x;
     o1 = col.y;
     o2 = col.z;
@@ -602,8 +572,9 @@ __global__ __launch_bounds__(64, 8) void k_sample(Frame F) {
 // frame's whole grid).  Production builds only.
 __device__ __forceinline__ void batch_slot(int& frame, int& rowslot) {
   const int L = blockIdx.z * gridDim.y + blockIdx.y, n = gridDim.z;
-  rowslot = L / n;
-  frame = L - rowslot * n;
+  // uniform: kept in SGPRs (the division is VALU code)
+  rowslot = __builtin_amdgcn_readfirstlane(L / n);
+  frame = __builtin_amdgcn_readfirstlane(L - rowslot * n);
 }
 #ifndef RM_KERNELS_AA_ONLY
 __global__ __launch_bounds__(64, 8) void k_pixel_frames(FrameBatch B) {

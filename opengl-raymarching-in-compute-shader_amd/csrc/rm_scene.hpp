@@ -681,7 +681,6 @@ __device__ __forceinline__ void lin_exit_b(f3 ro, float s0, float hmin, float& b
   b2 = ((ro.y + 5.5f) - s0 - hmin * HI) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
 }
 constexpr float SH_YTOP = 3.001f;  // >= the top of every bounded primitive (below)
-#if defined(RM_EXIT_YSLAB) || defined(RM_EXIT_PROJ)
 // Two more lower bounds of the five objects (round 5), each linear in t like the
 // ball's, so either one holding from t_j on proves the objects term as well:
 //   * the slab below SH_YTOP, which holds every bounded primitive (each reaches
@@ -711,7 +710,6 @@ __device__ __forceinline__ float lin_exit_b1p(f3 ro, f3 rd, float invl, float s0
   const float k = (SH_RALL + s0) + hmin;
   return (k - u) + 0x1p-17f * (e1 + k);
 }
-#endif
 __device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float s1, float b1, float b2,
                                             float b3 = __builtin_huge_valf()) {
   const float LO = 1.0f - 0x1p-12f;
@@ -721,7 +719,6 @@ __device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float
   const float a2 = (rdy - s1 - c) * LO - 0x1p-20f * (fabsf(rdy) + s1 + c);
   const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
   const float INF = __builtin_huge_valf();
-#if defined(RM_EXIT_YSLAB) || defined(RM_EXIT_PROJ)
   // b1 may be negative (the projection): T1 rounded up either way
   const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * (b1 >= 0.0f ? UP : DN);
   const float r2 = __builtin_amdgcn_rcpf(a2);
@@ -729,23 +726,14 @@ __device__ __forceinline__ float lin_exit_T(float c, float rdl, float rdy, float
   const float T3 = b3 * r2 * (b3 >= 0.0f ? UP : DN);  // +inf for b3 = +inf
   const float Tobj = a1 > 0.0f ? __builtin_fminf(T1, T3) : T3;
   return a2 > 0.0f ? __builtin_fmaxf(Tobj, T2) : INF;
-#else
-  const float T1 = b1 * __builtin_amdgcn_rcpf(a1) * UP;
-  const float T2 = -(b2 * __builtin_amdgcn_rcpf(a2) * (b2 >= 0.0f ? DN : UP));
-  return (a1 > 0.0f && a2 > 0.0f) ? __builtin_fmaxf(T1, T2) : INF;
-#endif
 }
 constexpr float MISS_C = 0.000001f * (1.0f + 0x1p-9f);
 __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd, float rdl) {
   const float s0 = ray_s0(ro);
-  float b1, b2, b3 = __builtin_huge_valf();
+  float b1, b2, b3;
   lin_exit_b(ro, s0, hmin, b1, b2);
-#ifdef RM_EXIT_PROJ
   b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, __builtin_amdgcn_rcpf(rdl), s0, hmin));
-#endif
-#ifdef RM_EXIT_YSLAB
   b3 = lin_exit_b3(ro.y, s0, hmin);
-#endif
   return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2, b3);
 }
 // c = Frame::shc, (1 + 2^-9) / k (1 + 2^-12) (0 for k = +inf): the host forms it

@@ -382,8 +382,22 @@ __device__ __forceinline__ float table_exit_T(const float* ex, float c, float hm
     const float rdl = __builtin_amdgcn_sqrtf(dot(rd, rd));
     const float a1 = (rdl * LO - s1 - c) * LO - 0x1p-20f * (rdl + c);
     const float b1 = (rc + ex[rm::EX_R] + s0 + hmin) * HI;
-    if (!(a1 > 0.0f)) return INF;
-    T = b1 * __builtin_amdgcn_rcpf(a1) * UP;
+    float To = a1 > 0.0f ? b1 * __builtin_amdgcn_rcpf(a1) * UP : INF;
+    // ... or the slab of their box along y (round 5, as rm_scene.hpp's slab below
+    // the objects): on the side of the box the ray leaves it by, every entry is
+    // at least (p.y - hi.y) (or lo.y - p.y) - slack, linear in t; the first of
+    // the bounds to hold for good proves the entries' term.  The x and z slabs
+    // cost more than they saved (reference-shaped table, cfg3: specialised
+    // +4.6 %, generic +1 %, profiles/r05_ab_tableslab.txt), as for the built-in.
+    {
+      const float r = rd.y, ra = fabsf(r), sc = s1 + c, sh = s0 + hmin;
+      const float edge = r > 0.0f ? ex[rm::EX_BOX + 4] : ex[rm::EX_BOX + 1];
+      const float as = (ra - sc) - 0x1p-20f * (ra + sc);
+      const float bs = ((r > 0.0f ? edge - ro.y : ro.y - edge) + sh) + 0x1p-20f * ((fabsf(edge) + fabsf(ro.y)) + sh);
+      if (as > 0.0f) To = __builtin_fminf(To, bs * __builtin_amdgcn_rcpf(as) * (bs >= 0.0f ? UP : DN));
+    }
+    if (!(To < INF)) return INF;
+    T = To;
   }
   const int np = (int)ex[rm::EX_NPLANES];
   for (int j = 0; j < np; ++j) {
@@ -1238,10 +1252,10 @@ __device__ __forceinline__ size_t out_index(const Frame& F, int tx, int ty, int 
 
 // main glsl:291-344 without AA: one lane per pixel, 8x8 pixels per wave.
 template <bool COUNT, int KL, int SL>
-__device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds) {
+__device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds, int rowslot) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x;
-  const int by = tile_row(blockIdx.y, gridDim.y);
+  const int by = tile_row(rowslot, gridDim.y);
   const int bx = tile_col(blockIdx.x, gridDim.x, 4);
   const int px = bx * 8 + (lane & 7);
   const int lrow = by * 8 + (lane >> 3);
@@ -1269,15 +1283,14 @@ __device__ __forceinline__ void table_pixel_body(const Frame& F, float* lds) {
 // samples of a pixel in adjacent lanes, summed in the reference's order
 // ((c0 + c1) + c2) + c3 before the / 4 (glsl:315-335).
 template <bool COUNT, int KL, int SL>
-__device__ __forceinline__ void table_sample_body(const Frame& F, float* lds) {
+__device__ __forceinline__ void table_sample_body(const Frame& F, float* lds, int rowslot) {
   const Table S = stage(F, lds);
   const int lane = threadIdx.x, s = lane & 3, q = lane >> 2;
-  const int by = tile_row(blockIdx.y, gridDim.y);
+  const int by = tile_row(rowslot, gridDim.y);
   const int bx = tile_col(blockIdx.x, gridDim.x, 8);
   const int px = bx * 4 + (q & 3);
   const int lrow = by * 4 + (q >> 2);
   if (px >= F.width || lrow >= F.rows) return;  // the 4 lanes of a pixel leave together
-  const size_t idx = (size_t)lrow * (size_t)F.width + (size_t)px;
   const int py = global_row(F, lrow);
   TCnt c = {0, 0, 0, 0, 0, 0};
   f3 col = mk(0.0f, 0.0f, 0.0f);
@@ -1314,31 +1327,42 @@ __device__ __forceinline__ void table_sample_body(const Frame& F, float* lds) {
 template <bool COUNT, int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel(Frame F) {
   extern __shared__ float lds[];
-  table_pixel_body<COUNT, KL, SL>(F, lds);
+  table_pixel_body<COUNT, KL, SL>(F, lds, blockIdx.y);
 }
 template <bool COUNT, int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample(Frame F) {
   extern __shared__ float lds[];
-  table_sample_body<COUNT, KL, SL>(F, lds);
+  table_sample_body<COUNT, KL, SL>(F, lds, blockIdx.y);
 }
 
 // Frame batches (rm_dispatch_frames): n frames of one table,
-// size and AA setting in one launch, grid.z = the frame, each workgroup reading
-// its frame's constants from the batch in the kernel arguments (as
-// k_sample_frames, rm_kernels.hip).  The bodies are the kernels' above, so every
-// frame is the image of its own dispatch.  Production kernels only (a batch
-// collects no counters).
+// size and AA setting in one launch, each workgroup reading its frame's
+// constants from the batch in the kernel arguments.  The (y, z) workgroup slots
+// are read row-major over the frames, as k_sample_frames reads them
+// (rm_kernels.hip batch_slot: every frame's slowest rows first).  The bodies are
+// the kernels' above, so every frame is the image of its own dispatch.
+// Production kernels only (a batch collects no counters).
+__device__ __forceinline__ void table_batch_slot(int& frame, int& rowslot) {
+  const int L = blockIdx.z * gridDim.y + blockIdx.y, n = gridDim.z;
+  // uniform: kept in SGPRs (the division is VALU code)
+  rowslot = __builtin_amdgcn_readfirstlane(L / n);
+  frame = __builtin_amdgcn_readfirstlane(L - rowslot * n);
+}
 template <int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_pixel_frames(
     FrameBatch B) {
   extern __shared__ float lds[];
-  table_pixel_body<false, KL, SL>(B.f[blockIdx.z], lds);
+  int f, r;
+  table_batch_slot(f, r);
+  table_pixel_body<false, KL, SL>(B.f[f], lds, r);
 }
 template <int KL = rm::EX_MAX_SLOTS, int SL = 0>
 __global__ __launch_bounds__(64, SL ? RM_TABLE_SL_WAVES : RM_TABLE_MIN_WAVES) void k_table_sample_frames(
     FrameBatch B) {
   extern __shared__ float lds[];
-  table_sample_body<false, KL, SL>(B.f[blockIdx.z], lds);
+  int f, r;
+  table_batch_slot(f, r);
+  table_sample_body<false, KL, SL>(B.f[f], lds, r);
 }
 
 }  // namespace rmd

@@ -15,7 +15,7 @@ from hypothesis import strategies as st  # noqa: E402
 
 TABLE_WORDS, TW_TYPE, TW_BALL = 24, 0, 20
 EX_VALID, EX_CX, EX_R, EX_NPLANES = 0, 1, 4, 7
-EX_LIP, EX_NSLOTS, EX_EVAL_MASK, EX_PLANE_MASK, EX_SLOTS, EXIT_WORDS = 24, 25, 26, 27, 28, 36
+EX_LIP, EX_NSLOTS, EX_EVAL_MASK, EX_PLANE_MASK, EX_SLOTS, EX_BOX, EXIT_WORDS = 24, 25, 26, 27, 28, 36, 42
 PLANE = 5
 
 f32_any = st.floats(width=32, allow_nan=True, allow_infinity=True)
@@ -127,7 +127,8 @@ def _sdf64(p, prim, blend):
 def test_culling_balls_bound_every_entry(rm, data):
     """A valid table's per-entry ball (TW_BALL) and the table's exit ball (EX_C, EX_R)
     are lower bounds of the entries' distances: dist_k(p) >= |p - c_k| - r_k and the
-    ball of every bounded entry lies inside the exit ball."""
+    ball of every bounded entry lies inside the exit ball; so is the exit box (EX_BOX,
+    the slab exits): dist_k(p) >= p_a - hi_a and lo_a - p_a on every axis."""
     prims = data.draw(finite_table(rm))
     w = _words(rm, prims)
     assert w is not None
@@ -139,6 +140,8 @@ def test_culling_balls_bound_every_entry(rm, data):
     rng = np.random.default_rng(data.draw(st.integers(0, 2 ** 32 - 1)))
     p = rng.uniform(-150, 150, (64, 3))
     C, R = hdr[EX_CX:EX_CX + 3], hdr[EX_R]
+    lo, hi = hdr[EX_BOX:EX_BOX + 3], hdr[EX_BOX + 3:EX_BOX + 6]
+    slab = np.maximum(p - hi, lo - p).max(-1)
     for k, prim in enumerate(prims):
         if prim.type == PLANE:
             continue
@@ -147,4 +150,6 @@ def test_culling_balls_bound_every_entry(rm, data):
         for d in _sdf64(p, prim, 0.5):
             ok = d >= lb - 1e-9 * (1.0 + np.abs(lb))
             assert ok.all(), (k, prim.type, (lb - d).max())
+            ok = d >= slab - 1e-9 * (1.0 + np.abs(slab))
+            assert ok.all(), (k, prim.type, (slab - d).max())
         assert np.sqrt(((ball[:3] - C) ** 2).sum()) + ball[3] <= R * (1 + 1e-6) + 1e-6, k
