@@ -569,17 +569,8 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       idp = (v <= m) ? k : idp;
       m = vmin(m, v);
     };
-#ifdef RM_RETEST_PROJ
-    // A downward ray moving away from k's ball leaves k above the plane for good:
-    // |p(t') - c| >= |rd| (t' - t) + u, u = rd.(p - c) / |rd|, while the plane
-    // drops by -rd.y (t' - t) and the slack grows by s1 (t' - t) <= |rd| (t' - t),
-    // so u > R + pl + slack (rounded: u / 2 from inv2v <= 1 / (2 |rd|), the second
-    // slack covering its float error) ends k's re-tests (te = +inf).
-    const float iu = rd.y <= 0.0f ? lc.inv2v : 0.0f;
-    const float hu = 0.5f * (pl + slack);
-#endif
     // re-test k; returns true when k must be evaluated exactly at this step
-    auto retest = [&](float x, float R, float& te, int k, float ox, float oy, float oz) -> bool {
+    auto retest = [&](float x, float R, float& te, int k) -> bool {
       RM_STAT(1);
       RM_STAT(16 + k);
       const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf(x), CULL_REL_LO, -(CULL_ABS + R));
@@ -592,12 +583,6 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       // max (a te below t may be negative) without t among its operands: a te
       // below t is as expired as te = t (round 3).
       te = vmax(__builtin_fmaf(lb - pl, invp, t), te);
-#ifdef RM_RETEST_PROJ
-      const float u2 = __builtin_fmaf(rd.x, ox, __builtin_fmaf(rd.y, oy, rd.z * oz)) * iu;
-      te = u2 > __builtin_fmaf(0.5f, R, hu) ? __builtin_huge_valf() : te;
-#else
-      (void)ox, (void)oy, (void)oz;
-#endif
       // Evaluate exactly when the new expiry does not pass t: an expired lane
       // whose gap is <= 0, and also one whose tiny gap > 0 cannot move t -- an
       // extra exact evaluation, never a wrong skip.  One compare instead of two
@@ -614,35 +599,35 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
     const bool GRP = __any(t >= lc.tegrp);
     if (GRP && __any(t >= lc.te[0])) {  // sphere (15,0,-10) r3, glsl:111
       const float x0 = (o.ax * o.ax + o.ay2) + o.az2;
-      if (retest(x0, 3.0f, lc.te[0], 0, o.ax, o.ay, o.az)) {
+      if (retest(x0, 3.0f, lc.te[0], 0)) {
         RM_STAT(10);
         take(sqrt_core(x0) - 3.0f, 0);
       }
     }
     if (GRP && __any(t >= lc.te[1])) {  // sphere (-25,0,-10) r3, glsl:112
       const float x1 = (o.bx * o.bx + o.ay2) + o.az2;
-      if (retest(x1, 3.0f, lc.te[1], 1, o.bx, o.ay, o.az)) {
+      if (retest(x1, 3.0f, lc.te[1], 1)) {
         RM_STAT(11);
         take(sqrt_core(x1) - 3.0f, 1);
       }
     }
     if (GRP && __any(t >= lc.te[2])) {  // box/sphere blend, glsl:115-117
       const float xs = (o.cx2 + o.ay2) + o.az2;
-      if (retest(xs, R_BLEND_LO, lc.te[2], 2, o.cx, o.ay, o.az)) {
+      if (retest(xs, R_BLEND_LO, lc.te[2], 2)) {
         RM_STAT(12);
         take(sd_blend(o, xs, blend, omblend), 4);
       }
     }
     if (__any(t >= lc.te[3])) {  // torus, glsl:119
       const float tz = p.z - 10.0f;
-      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3, o.cx, o.ay, tz)) {
+      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
         RM_STAT(13);
         take(sd_torus(o, tz), 5);
       }
     }
     if (GRP && __any(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
-      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4, kx, ky, kz)) {
+      if (retest((kx * kx + ky * ky) + kz * kz, R_CAPSULE, lc.te[4], 4)) {
         RM_STAT(14);
         take(sd_capsule(o, p), 6);
       }
