@@ -732,7 +732,9 @@ __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd
   const float s0 = ray_s0(ro);
   float b1, b2, b3;
   lin_exit_b(ro, s0, hmin, b1, b2);
-  b1 = __builtin_fminf(b1, lin_exit_b1p(ro, rd, __builtin_amdgcn_rcpf(rdl), s0, hmin));
+  // the slab, not the projection: shadow rays rise from the floor toward the light,
+  // and the projection's ~8 VALU per call saved nothing (cfg3 -0.6 % without it,
+  // profiles/r05_ab_shadow_noproj.txt)
   b3 = lin_exit_b3(ro.y, s0, hmin);
   return lin_exit_T(c, rdl, rd.y, ray_s1(rdl), b1, b2, b3);
 }
