@@ -619,11 +619,20 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
       }
     }
     if (__any(t >= lc.te[3])) {  // torus, glsl:119
+      // Evaluated exactly instead of re-tested against its ball (round 5): most
+      // torus re-tests ended in the evaluation anyway (6.55 of 8.0 per wave, cfg3
+      // frame 60), so the ball's v_sqrt and compare were extra work.  The exact
+      // value serves as the budget's lower bound (its float error is far inside
+      // the slack), and taking it for a lane that did not need it is what the
+      // reference's opU does (it evaluates everything).  -2.9 % per cfg3 frame
+      // (with the tegrp change below; profiles/r05_ab_tegrp_torus.txt).
+      RM_STAT(1);
+      RM_STAT(16 + 3);
+      RM_STAT(13);
       const float tz = p.z - 10.0f;
-      if (retest((o.cx2 + o.ay2) + tz * tz, R_TORUS, lc.te[3], 3)) {
-        RM_STAT(13);
-        take(sd_torus(o, tz), 5);
-      }
+      const float v = sd_torus(o, tz);
+      take(v, 5);
+      lc.te[3] = vmax(__builtin_fmaf(v - pl, invp, t), lc.te[3]);
     }
     if (GRP && __any(t >= lc.te[4])) {  // capsule, glsl:120
       const float kx = p.x - CAP_MX, ky = p.y - CAP_MY, kz = p.z - CAP_MZ;
@@ -632,7 +641,9 @@ __device__ __forceinline__ float scene_lazy(f3 ro, f3 rd, float t, LazyCull& lc,
         take(sd_capsule(o, p), 6);
       }
     }
-    lc.tegrp = vmin(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[4]);
+    // a block entered for the torus alone changed no other expiry: tegrp stands
+    // (two v_min fewer, wave-uniform branch)
+    if (GRP) lc.tegrp = vmin(vmin3(lc.te[0], lc.te[1], lc.te[2]), lc.te[4]);
     lc.temin = vmin(lc.tegrp, lc.te[3]);
     lc.idb = idp;  // (the plane's tie rule and the step: lazy_id)
   }
