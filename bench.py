@@ -74,7 +74,7 @@ SWEEP_FRAMES = 120
 # frame times of DESIGN §9): --rank0-share -1 gives rank 0 the rows per round that
 # balance its render + assembly against the other ranks' render
 # (rm.best_rank0_rows).
-ASSEMBLE_RATIO = {1: 0.53, 2: 0.077, 3: 0.0141, 4: 0.0130, 5: 0.0153}  # round 5 frame times
+ASSEMBLE_RATIO = {1: 0.57, 2: 0.079, 3: 0.0145, 4: 0.0134, 5: 0.0158}  # round 5 frame times
 
 
 def bench_frames(steps: int) -> list:
