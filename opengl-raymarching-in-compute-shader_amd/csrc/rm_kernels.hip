@@ -300,7 +300,7 @@ __device__ __forceinline__ float softshadow_impl(const Frame& F, f3 ro, f3 rd, f
   float res = 1.0f, t = 0.0f;
   int dummy;
   RM_STAT(29);
-  const float ex = shadow_exit_init(F.shc, ro, rd, rdl);
+  const float ex = shadow_exit_init(F.shc, ro, rd, rdl, light_in_ball(F));
   for (int i = 0; i < 16; ++i) {
     if (lin_exit(ex, t)) {  // the remaining steps are no-ops
       if (COUNT) c.shadow += 16 - i;

@@ -757,8 +757,28 @@ __device__ __forceinline__ float lin_exit_init(float c, float hmin, f3 ro, f3 rd
 // length the light term at the same pos has already formed (point_light's
 // `distance`, correctly rounded): the caller passes it instead of a v_sqrt
 // (round 4).
-__device__ __forceinline__ float shadow_exit_init(float c, f3 ro, f3 rd, float rdl) {
-  return lin_exit_init(c, 0.001f, ro, rd, rdl);
+// lpos_in_ball: the light lies within the objects' ball (|light - C| <= R_ALL; a
+// uniform of the frame, so a wave-uniform branch).  Then every shadow ray has
+// |rd| = |light - ro| <= |ro - C| + R_ALL, and the ball's bound holds only past
+// t = 1, the light: the exit takes the plane and the object slab alone, without
+// the ball's v_sqrt and v_rcp (cfg3 -0.8 % per frame, the sweep's light at
+// (-5, 5, -10); profiles/r05_ab_shadow_slab.txt).
+__device__ __forceinline__ float shadow_exit_init(float c, f3 ro, f3 rd, float rdl, bool lpos_in_ball) {
+  if (!lpos_in_ball) return lin_exit_init(c, 0.001f, ro, rd, rdl);
+  const float s0 = ray_s0(ro), s1 = ray_s1(rdl), hmin = 0.001f;
+  const float b2 = ((ro.y + 5.5f) - s0 - hmin * (1.0f + 0x1p-12f)) - 0x1p-19f * (fabsf(ro.y) + 5.5f + hmin + s0);
+  const float b3 = lin_exit_b3(ro.y, s0, hmin);
+  const float a2 = (rd.y - s1 - c) * (1.0f - 0x1p-12f) - 0x1p-20f * (fabsf(rd.y) + s1 + c);
+  const float UP = 1.0f + 0x1p-20f, DN = 1.0f - 0x1p-20f;
+  const float r2 = __builtin_amdgcn_rcpf(a2);
+  const float T2 = -(b2 * r2 * (b2 >= 0.0f ? DN : UP));
+  const float T3 = b3 * r2 * (b3 >= 0.0f ? UP : DN);
+  return a2 > 0.0f ? __builtin_fmaxf(T3, T2) : __builtin_huge_valf();
+}
+// |light - C| <= R_ALL (rounded toward "outside": a light at the boundary keeps the ball)
+__device__ __forceinline__ bool light_in_ball(const Frame& F) {
+  const float ex = F.lpos[0] - SH_CX, ey = F.lpos[1] - SH_CY, ez = F.lpos[2] - SH_CZ;
+  return (ex * ex + ey * ey) + ez * ez <= SH_RALL * SH_RALL * (1.0f - 0x1p-10f);
 }
 __device__ __forceinline__ float miss_exit_init(f3 ro, f3 rd) { return lin_exit_init(MISS_C, 0.0f, ro, rd, ray_rdl(rd)); }
 __device__ __forceinline__ bool lin_exit(float T, float t) { return t > T; }
