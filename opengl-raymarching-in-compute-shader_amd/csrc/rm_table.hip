@@ -706,6 +706,17 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
       #pragma unroll
       for (int j = 0; j < KL; ++j) {
         if (j >= ns || !wany(tt >= lz.te[j])) continue;
+#ifdef RM_TABLE_STATIC  // (the specialised kernels: the type is known at compile time)
+        if (S.type(j) == RM_PRIM_TORUS) {
+          // evaluated instead of re-tested, as the built-in march does (rm_scene.hpp
+          // scene_lazy): the exact value is the budget's lower bound
+          const float v = prim_dist<kBoundedPoints>(S.entry(j), RM_PRIM_TORUS, p, S.blend, S.omblend);
+          idp = (v <= m) ? j : idp;
+          m = vmin(m, v);
+          lz.te[j] = vmax(__builtin_fmaf(v - pl, lz.invp, tt), lz.te[j]);
+          continue;
+        }
+#endif
 #ifdef RM_TABLE_STATIC
         const float* B = S.entry(j) + rm::TW_BALL;
 #else
