@@ -128,6 +128,15 @@ STRESS = [
     ("cam_x_3e9", None, (3.0e9, 0.0, 15.0)),
     ("cam_x_-3e9", None, (-3.0e9, 0.0, 15.0)),
     ("cam_z_3e9", None, (0.0, 0.0, 3.0e9)),
+    # the round-5 exit bounds at their edges (rm_scene.hpp lin_exit_b3 / b1p,
+    # shadow_exit_init): the camera on and above the objects' slab y <= 3.001,
+    # the light just inside and just outside the objects' ball (R_ALL = 23.001
+    # around (-5, 0, -10)), and a low light far outside it
+    ("cam_on_slab", None, (0.0, 3.0, 15.0)),
+    ("cam_above_slab", None, (2.0, 6.0, 14.0)),
+    ("light_ball_inside", (-5.0, 22.9, -10.0), None),
+    ("light_ball_outside", (-5.0, 23.1, -10.0), None),
+    ("light_low_far", (100.0, 1.0, 100.0), None),
 ]
 
 
