@@ -14,6 +14,12 @@ shadows, 4x supersampling, 1 MI355X.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1..5]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+--gpus N > 1 without a launcher (no WORLD_SIZE in the environment) runs the same
+sharded, RCCL-gathered step in this one process over N devices (librm's
+rm_config.ngpus contexts: one shard per device, a single-process communicator,
+the gather and rank 0's assembly inside librm); with fewer than N visible devices
+it exits with status 2.
+
 Step k of K renders sweep frame floor(k * 120 / K): every run samples the whole
 sweep evenly, so `value` is the sweep mean.
 
@@ -212,7 +218,7 @@ def comm_ids(n: int, rank: int) -> list:
     return ids
 
 
-def default_batch(config: int, dist_on: bool, one_comm: bool, steps: int) -> int:
+def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int:
     """Frames per launch when --batch is not given (measured).
 
     One GPU: cfg1 / cfg2 frames (4K / 32K one-wave workgroups) are shorter than their
@@ -223,14 +229,31 @@ def default_batch(config: int, dist_on: bool, one_comm: bool, steps: int) -> int
     still spread over the 3 contexts.  The 4K supersampled frames fill the chip by
     themselves: pairs of frames on 4 contexts measure 0.8 % faster than single frames
     on 3 (0.8193 against 0.8258 ms, 7 interleaved rounds, profiles/r04_inflight.txt);
-    the 8K graph-replayed frames (cfg5) stay single, 3 in flight."""
+    the 8K graph-replayed frames (cfg5) stay single, 3 in flight.
+
+    N > 1: pairs of frames per launch on 2 contexts (round 6, tools/probe_scale.py,
+    profiles/r06_scale.txt): a rank's 1/N share of a frame is shorter than its
+    longest waves, so single-frame launches left the SIMDs idle behind them (N = 8:
+    4.4x one GPU on 4 contexts); pairs on 2 contexts give ~6.9x at N = 8 in the
+    probe with either stream placement, and a launch's gather starts as soon as its
+    two frames are done (larger batches gather more bytes after the last render)."""
     if one_comm:
         return 4  # N > 1, one communicator: gather batch j while batch j + 1 renders
-    if dist_on:
-        return 1
+    if sharded:
+        return 2
     if config in (1, 2):
         return max(1, min(20, -(-steps // 3)))
     return 2 if config in (3, 4) else 1
+
+
+def _gather_objects(mine, ws):
+    """Every rank's `mine` (torch.distributed over gloo), or [mine] in one process."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [mine]
+    allp = [None] * ws
+    dist.all_gather_object(allp, mine)
+    return allp
 
 
 def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
@@ -238,7 +261,6 @@ def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
     render kernel, the ncclGather and rank 0's assembly) over EVERY timed frame, re-rendered
     eagerly after the timed region (one frame, or one batch, at a time), so a scaling
     shortfall can be attributed to render imbalance or to the gather."""
-    import torch.distributed as dist
     vals = {"render_ms": [], "gather_ms": [], "assemble_ms": []}
     r.enable_timing(True)
     for i in range(0, len(frames), batch):
@@ -257,8 +279,7 @@ def frame_phase_stats(r, frames, uniforms, batch, rank, ws):
     for k, v in vals.items():
         mine[k.replace("_ms", "_mean_ms")] = round(float(np.mean(v)), 4)
         mine[k.replace("_ms", "_max_ms")] = round(float(np.max(v)), 4)
-    allp = [None] * ws
-    dist.all_gather_object(allp, mine)
+    allp = _gather_objects(mine, ws)
     return {"per_rank": allp,
             "frames": len(frames), "frames_per_sample": batch,
             "max_render_mean_ms": max(p["render_mean_ms"] for p in allp),
@@ -280,15 +301,34 @@ def rccl_report(rs, rank, ws):
     """What RCCL itself reports for every communicator of every rank (ncclCommCount,
     ncclCommUserRank, ncclCommCuDevice, ncclGetVersion via rm_comm_rccl_info): the line
     proves how many ranks RCCL formed, not only torch's WORLD_SIZE."""
-    import torch.distributed as dist
     mine = {"rank": rank, "comms": [rj.rccl_info() for rj in rs]}
-    allr = [None] * ws
-    dist.all_gather_object(allr, mine)
+    allr = _gather_objects(mine, ws)
     counts = sorted({c["count"] for p in allr for c in p["comms"]})
+    # (one process over N devices: rm_comm_rccl_info checks every device's member
+    # communicator against its user rank and device, and reports device 0's)
     ok = all(c["count"] == ws and c["user_rank"] == p["rank"] for p in allr for c in p["comms"])
     return {"version": allr[0]["comms"][0]["version"] if allr[0]["comms"] else None,
             "nranks_seen": counts, "world_size": ws, "all_communicators_match": ok,
             "per_rank": allr}
+
+
+def run_mode(gpus: int, launched: bool, ws: int, single_process: bool):
+    """How bench.py runs --gpus N: ("launcher", None) under torch.distributed.run
+    (one process per GPU, WORLD_SIZE set); ("single_process", None) without a
+    launcher when N > 1 or --single-process (every device in this process, librm's
+    rm_config.ngpus contexts); ("single_gpu", None) for N = 1; ("error", why) for a
+    launcher whose world size is not N, or N < 1."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    if launched:
+        if ws != gpus:
+            return "error", f"launched with WORLD_SIZE={ws} but --gpus {gpus}"
+        if single_process:
+            return "error", "--single-process runs without a launcher"
+        return "launcher", None
+    if gpus > 1 or single_process:
+        return "single_process", None
+    return "single_gpu", None
 
 
 def dist_env():
@@ -306,6 +346,10 @@ def main() -> int:
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--row-block", type=int, default=8,
                     help="rows per interleaved block when sharding over ranks")
+    ap.add_argument("--single-process", action="store_true",
+                    help="the sharded, RCCL-gathered step over --gpus devices in this one process "
+                         "(rm_config.ngpus), also at --gpus 1; the default when --gpus N > 1 runs "
+                         "without a launcher")
     ap.add_argument("--rank0-share", type=float, default=-1.0,
                     help="N > 1: rank 0's rows per round as a share of --row-block (rank 0 also "
                          "assembles every frame, so it renders fewer rows: rm_config.rank0_rows = "
@@ -318,8 +362,8 @@ def main() -> int:
                     help="frames in flight: consecutive frames render from separate contexts on "
                          "separate streams, so frame f+1's waves fill the SIMDs that frame f's "
                          "last long waves leave idle (1 = one context, frames in turn; "
-                         "0 = 3 on one GPU, 4 on a sharded frame, whose per-rank share is "
-                         "shorter than its longest waves)")
+                         "0 = 3 on one GPU (4 for the 4K pairs), 2 on a sharded frame, each "
+                         "launch two frames)")
     ap.add_argument("--batch", type=int, default=-1,
                     help="frames per launch (rm_dispatch_frames: one grid over B frames, so frame "
                          "k+1's waves fill the SIMDs frame k's longest waves leave idle); 1 = one "
@@ -364,11 +408,20 @@ def main() -> int:
     # step even at world size 1, so one GPU runs the driver's N > 1 code path and its
     # RCCL calls (communicator, gather, assembly inside librm) on hardware
     dist_on = ws > 1 or os.environ.get("RM_BENCH_FORCE_DIST") == "1"
-    if ws != args.gpus:
-        if ws == 1 and args.gpus > 1:
-            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run",
-                  file=sys.stderr)
+    # --gpus N without a launcher: every device in this process (rm_config.ngpus)
+    mode, why = run_mode(args.gpus, "WORLD_SIZE" in os.environ, ws, args.single_process)
+    if mode == "error":
+        print(f"bench.py: {why}", file=sys.stderr)
+        return 2
+    single = mode == "single_process"
+    if single:
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} in one process needs {args.gpus} visible devices, "
+                  f"this host shows {ndev}", file=sys.stderr)
             return 2
+    sharded = dist_on or single
+    nsh = ws if dist_on else (args.gpus if single else 1)  # shards of every frame
     torch.cuda.set_device(local)
     if dist_on:
         # host-side control only (RCCL ids, barriers, the max over ranks of the time):
@@ -383,13 +436,15 @@ def main() -> int:
     # Frames in flight: consecutive frames go to separate contexts, each with its own
     # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
     # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
-    one_comm = dist_on and args.comms == 1
-    batch = args.batch if args.batch > 0 else default_batch(args.config, dist_on, one_comm, args.steps)
+    one_comm = sharded and args.comms == 1
+    batch = args.batch if args.batch > 0 else default_batch(args.config, sharded, one_comm, args.steps)
     batch = max(1, min(batch, rm.RM_MAX_BATCH, args.steps))
-    # contexts in flight: 3 frames or batches on one GPU (4 for the 4K pairs), 4
-    # frames of a sharded step
-    nfl = args.inflight if args.inflight > 0 else (4 if dist_on or (batch == 2 and args.config in (3, 4)) else 3)
-    nfl = nfl if (not dist_on or args.pipeline) else 1
+    if use_graph:
+        batch = 1  # a graph replays one frame
+    # contexts in flight: 3 frames or batches on one GPU (4 for the 4K pairs), 2
+    # batches of a sharded step (default_batch)
+    nfl = args.inflight if args.inflight > 0 else (2 if sharded else (4 if batch == 2 and args.config in (3, 4) else 3))
+    nfl = nfl if (not sharded or args.pipeline) else 1
     if one_comm:
         nfl = 1  # one context, one communicator; batches overlap through its gather stream
 
@@ -403,13 +458,28 @@ def main() -> int:
             ucache[f] = rm.sweep_uniforms(f, SWEEP_FRAMES, cfg["bounces"], cfg["aa"], cfg["shadow"])
         return ucache[f]
 
+    scene = rm.default_scene() if args.scene in ("table", "table-spec") else None
+    spec = args.scene == "table-spec"
     # the weighted interleave (rm_config.rank0_rows, rm_shard.hpp): rank 0's rows per round
     if args.rank0_share > 0:
         rank0_rows = max(1, int(round(args.rank0_share * args.row_block)))
+        rank0_src = f"--rank0-share {args.rank0_share}"
+    elif nsh > 1 and scene is None:
+        rank0_rows = rm.best_rank0_rows(args.row_block, nsh, ASSEMBLE_RATIO[args.config])
+        rank0_src = (f"rm.best_rank0_rows(row_block, N, ASSEMBLE_RATIO[{args.config}] = "
+                     f"{ASSEMBLE_RATIO[args.config]}): k_unshard time over the built-in scene's one-GPU "
+                     "frame time, tools/probe_unshard.py")
     else:
-        rank0_rows = rm.best_rank0_rows(args.row_block, ws, ASSEMBLE_RATIO[args.config]) if ws > 1 else 0
-    shard_args = (dict(row_block=args.row_block, shard=rank, nshards=ws, rank0_rows=rank0_rows)
-                  if dist_on else {})
+        #  the assembly ratio was measured for the built-in scene's frame
+        # time: a runtime table renders slower, so it keeps the plain interleave
+        rank0_rows = 0
+        rank0_src = "plain interleave" + (" (scene table)" if nsh > 1 else "")
+    if dist_on:
+        shard_args = dict(row_block=args.row_block, shard=rank, nshards=ws, rank0_rows=rank0_rows)
+    elif single:
+        shard_args = dict(row_block=args.row_block, ngpus=nsh, rank0_rows=rank0_rows)
+    else:
+        shard_args = {}
     rs = [rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local, **shard_args)
           for _ in range(nfl)]
     if dist_on:
@@ -417,8 +487,6 @@ def main() -> int:
         # ids, the host channel carries them; every rank joins in the same order
         for rj, cid in zip(rs, comm_ids(nfl, rank)):
             rj.comm_init(cid, ws, rank)
-    scene = rm.default_scene() if args.scene in ("table", "table-spec") else None
-    spec = args.scene == "table-spec"
 
     def use_scene(rj):
         if spec:
@@ -465,15 +533,21 @@ def main() -> int:
             nstep[0] += 1
             rs[j].dispatch_frames(barr[key])
 
+    devs = list(range(local, local + nsh)) if single else [local]
+
+    def sync_devices():
+        for d in devs:  # the device(s): every librm stream
+            torch.cuda.synchronize(d)
+
     def barrier():
         # librm's own wait first: on a communicator context it is bounded
         # (rm_comm_set_timeout) and turns a hung gather into RM_ERR_COMM
         for rj in rs:
             rj.synchronize()
-        torch.cuda.synchronize()  # the device: every librm stream
+        sync_devices()
         if dist_on:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync_devices()
 
     frames_timed = bench_frames(args.steps)
     # ---- spin-up (untimed): sustained load until the GPU's clocks have ramped ----
@@ -488,7 +562,7 @@ def main() -> int:
                 k += n
             for rj in rs:
                 rj.synchronize()
-            torch.cuda.synchronize()
+            sync_devices()
             more = (time.perf_counter() - s0) * 1e3 < args.spinup_ms
             if dist_on:
                 flag = torch.tensor([1 if more else 0], dtype=torch.int32)
@@ -522,7 +596,7 @@ def main() -> int:
     # over ranks below takes the slowest rank's end.
     for rj in rs:
         rj.synchronize()
-    torch.cuda.synchronize()
+    sync_devices()
     t1 = time.perf_counter()
     barrier()
     kernel_ms, launches = 0.0, 0
@@ -534,7 +608,7 @@ def main() -> int:
     kernel_time_basis = "HIP events on the launch stream over the timed region"
     batched = batch > 1 and not use_graph
     mean_launch_ms = None
-    if nfl > 1 or batch > 1 or (use_graph and dist_on):
+    if nfl > 1 or batch > 1 or (use_graph and sharded):
         # Overlapping frames stretch each launch's event interval (and on a
         # communicator context a graph launch holds the gather and the assembly
         # too), so the roofline takes its kernel time from the same frames rendered
@@ -565,10 +639,13 @@ def main() -> int:
     elapsed = t1 - t0
     phases = None
     rccl = None
-    if dist_on:
-        phases = frame_phase_stats(r, frames_timed, uniforms, batch if one_comm else 1, rank, ws)
+    if sharded:
+        phases = frame_phase_stats(r, frames_timed, uniforms, batch if batched else 1, rank, ws)
+        if single:
+            phases["note"] += ("; one process over N devices: rm_frame_phases reports device 0 "
+                               "(rank 0's render, the grouped gather, the assembly)")
         barrier()
-        rccl = rccl_report(rs, rank, ws)
+        rccl = rccl_report(rs, rank, nsh if single else ws)
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -579,9 +656,10 @@ def main() -> int:
     # ---- work counters of exactly the frames timed (untimed pass) ----
     ops_total = 0
     cnt_total = None
+    # (the timed kernel's share of the frame: this rank's shard, device 0's in one process)
     with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, counters=True, device=local,
-                     row_block=args.row_block if dist_on else 0, shard=rank if dist_on else 0,
-                     nshards=ws, rank0_rows=rank0_rows if dist_on else 0) as rc:
+                     row_block=args.row_block if sharded else 0, shard=rank if dist_on else 0,
+                     nshards=nsh, rank0_rows=rank0_rows if sharded else 0) as rc:
         if scene is not None:
             use_scene(rc)
         seen = {}
@@ -607,26 +685,48 @@ def main() -> int:
     # here, against the lane-instruction peak: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz
     # x 2 (dual issue) = 157.3 T FP32 ops/s counting an FMA as 2 -> 78.65 T
     # lane-instructions/s.  frac = SQ_INSTS_VALU x 64 / kernel time / 78.65 T.
-    valu_insts = pmc.get("SQ_INSTS_VALU") if pmc else None
+    valu_frame = pmc.get("SQ_INSTS_VALU") if pmc else None  # the whole frame's, per frame
+    # the timed kernel renders this rank's shard (device 0's in one process): the
+    # frame's instructions in proportion to its rows (an estimate; PMC passes are
+    # one-GPU whole frames)
+    share = (rm.shard_rows(H, args.row_block, nsh, 0 if single else rank, rank0_rows)[0] / H
+             if sharded and nsh > 1 else 1.0)
+    valu_insts = valu_frame * share if valu_frame else None
     valu_issue = (valu_insts * 64 / (mean_kernel_ms * 1e-3) / 1e12) if valu_insts else None
+    # the same instructions per frame of the timed region's throughput over the whole
+    # job's GPUs: frames overlap on several contexts, so this is
+    # the utilisation the measured value implies
+    valu_tput = (valu_frame * 64 / (elapsed / frames) / 1e12 / max(nsh, 1)) if valu_frame else None
     # The same kernel against the SIMDs' VALU issue slots: its busy slots per launch
     # (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2, committed PMC pass) per second of
     # the kernel time measured here, over 614.4 G slots/s.
-    busy_quads = pmc.get("valu_busy_quads") if pmc else None
+    busy_frame = pmc.get("valu_busy_quads") if pmc else None
+    busy_quads = busy_frame * share if busy_frame else None
     issue_rate = (busy_quads / (mean_kernel_ms * 1e-3) / 1e9) if busy_quads else None
     # ... and per frame of the timed region's throughput (frames in flight / batched)
-    issue_tput = (busy_quads / (elapsed / frames) / 1e9) if busy_quads else None
+    issue_tput = (busy_frame / (elapsed / frames) / 1e9 / max(nsh, 1)) if busy_frame else None
+    ms_step = elapsed / frames * 1e3
+    overlap_note = None
+    if mean_kernel_ms > ms_step:
+        overlap_note = (f"the kernel's own time per frame ({mean_kernel_ms:.4f} ms, launches timed one at a "
+                        f"time) exceeds ms_per_step ({ms_step:.4f} ms): in the timed region {nfl} contexts "
+                        "overlap their launches, so the next launch's waves fill the SIMDs a launch's last "
+                        "long waves leave idle and a frame's share of the wall clock is shorter than one "
+                        "launch's duration; frac_throughput is the utilisation at the measured value")
     # The reference's brute-force work (SURVEY 8(d) op weights x the exact counters of
     # the frames timed): the kernel skips most of it by proof, so this rate is not
     # hardware utilisation and can exceed the peak.
     achieved_tflops = ops_total / max(launches, 1) / (mean_kernel_ms * 1e-3) / 1e12
-    bytes_per_launch = (rm.shard_rows_cap(H, args.row_block, ws, rank0_rows) if dist_on else H) * W * 4
+    # algorithmic bytes of the timed kernel's image: RGBA8, or a gathered shard's packed
+    # RGB (rm_config.shard_format AUTO on a communicator context)
+    bytes_per_launch = (rm.shard_rows_cap(H, args.row_block, nsh, rank0_rows) * W * 3 if sharded
+                        else H * W * 4)
     hbm_gbs = bytes_per_launch / (mean_kernel_ms * 1e-3) / 1e9
 
     # ---- CPU baseline + parity sample (rank 0, N = 1 only) ----
     cpu = None
     parity = None
-    if rank == 0 and not dist_on and not args.no_cpu_baseline:
+    if rank == 0 and not sharded and not args.no_cpu_baseline:
         cpu, ref, rows = cpu_baseline(args, cfg, uniforms(frames_timed[-1]), frames_timed[-1])
         # GPU frame of the same sweep frame: the last step rendered it into its context's buffer.
         torch.cuda.synchronize()
@@ -636,8 +736,8 @@ def main() -> int:
                   "pixels_checked": int(d.shape[0] * d.shape[1]), "reference": "CPU oracle"}
 
     # ---- N > 1: the assembled frame of the last step against a single-GPU render ----
-    if dist_on and rank == 0:
-        torch.cuda.synchronize()
+    if sharded and rank == 0:
+        sync_devices()
         last = frames_timed[-1]
         with rm.Renderer(W, H, outputs=rm.RM_OUT_RGBA8, kernel=kernel, device=local) as rf:
             if scene is not None:
@@ -655,7 +755,7 @@ def main() -> int:
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mpixels/s",
-            "n_gpus": ws,
+            "n_gpus": nsh if sharded else ws,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / frames * 1e3, 4),
@@ -673,13 +773,18 @@ def main() -> int:
                        "contexts_in_flight": nfl,
                        "frames_per_launch": batch if batched else 1,
                        "frames_in_flight": nfl * (batch if batched else 1),
-                       "communicators_per_rank": (1 if one_comm else nfl) if dist_on else 0,
-                       "parallelism": (f"row-blocks of {args.row_block} x {ws} GPUs + RCCL gather"
+                       "communicators_per_rank": (1 if one_comm else nfl) if sharded else 0,
+                       "parallelism": (f"row-blocks of {args.row_block} x {nsh} GPUs + RCCL gather"
                                        + (" (pipelined)" if args.pipeline else "")
-                                       if dist_on else "single GPU"),
-                       "rank0_rows_per_round": (rank0_rows or args.row_block) if dist_on else None,
-                       "rows_per_rank": ([rm.shard_rows(H, args.row_block, ws, s_, rank0_rows)[0]
-                                          for s_ in range(ws)] if dist_on else None)},
+                                       + (", one process (rm_config.ngpus)" if single
+                                          else ", one process per GPU (rm_comm_init)")
+                                       if sharded else "single GPU"),
+                       "rank0_rows_per_round": (rank0_rows or args.row_block) if sharded else None,
+                       "rank0_rows_source": rank0_src if sharded else None,
+                       "shard_format": ("RGB8: 3 B per pixel gathered, alpha 255 restored by k_unshard "
+                                        "(rm_config.shard_format AUTO)") if sharded else None,
+                       "rows_per_rank": ([rm.shard_rows(H, args.row_block, nsh, s_, rank0_rows)[0]
+                                          for s_ in range(nsh)] if sharded else None)},
             "fps": round(frames / elapsed, 3),
             # host time to issue the K steps (rank 0): well below ms_per_step = GPU-bound
             "host_issue_ms_per_step": round((t_issue - t0) / args.steps * 1e3, 4),
@@ -688,8 +793,17 @@ def main() -> int:
                          "achieved": round(valu_issue, 3) if valu_issue else None,
                          "peak": VALU_LANE_PEAK_T, "unit": "T VALU lane-instructions/s",
                          "frac": round(valu_issue / VALU_LANE_PEAK_T, 4) if valu_issue else None,
+                         "frac_throughput": round(valu_tput / VALU_LANE_PEAK_T, 4) if valu_tput else None,
+                         "achieved_throughput": round(valu_tput, 3) if valu_tput else None,
+                         "frac_note": ("frac: executed VALU lane-instructions per frame (PMC) over the "
+                                       "kernel's own time per frame; frac_throughput: the same "
+                                       "instructions over ms_per_step" + (" and the N GPUs; at N > 1 "
+                                       "the shard's instructions are the frame's in proportion to its "
+                                       "rows" if sharded and nsh > 1 else "")),
+                         "kernel_time_vs_step": overlap_note,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "valu_insts_per_launch": valu_insts, "pmc_frames": pmc_frames(traffic_src),
+                         "valu_insts_per_launch": valu_insts, "valu_insts_per_frame": valu_frame,
+                         "pmc_frames": pmc_frames(traffic_src),
                          "kernel": kname, "mean_kernel_ms": round(mean_kernel_ms, 4),
                          "mean_launch_ms": round(mean_launch_ms, 4) if mean_launch_ms else None,
                          "per": "frame" + (f" (launches of {batch} frames: PMC values, kernel time and "

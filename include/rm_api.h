@@ -36,8 +36,8 @@
 extern "C" {
 #endif
 
-#define RM_API_VERSION 5
-#define RM_CONFIG_MAGIC 0x35434D52u /* "RMC5" little-endian: rm_config layout of API version 5 */
+#define RM_API_VERSION 6
+#define RM_CONFIG_MAGIC 0x36434D52u /* "RMC6" little-endian: rm_config layout of API version 6 */
 
 /* ---- status codes --------------------------------------------------------- */
 #define RM_OK 0
@@ -55,6 +55,16 @@ extern "C" {
 /* ---- output image formats (bitmask for rm_config.outputs) ----------------- */
 #define RM_OUT_RGBA8 1   /* display format (what the quad shows, Quad.glsl:21-25) */
 #define RM_OUT_RGBA32F 2 /* the reference texture's true storage (texture.cpp:19) */
+
+/* ---- RGBA8 shard image formats (rm_config.shard_format, API version 6) ----
+ * The reference stores alpha = 1.0 in every pixel (finalColor = vec4(render(),
+ * 1.0), and the mean of four such, computeShader.glsl:314-341), so a shard that
+ * travels to rank 0 need not carry it: an RGB8 shard image is [rows_cap][width]
+ * x 3 bytes (R, G, B), and the un-shard writes alpha 255.  The assembled frame
+ * is the same RGBA8 image byte for byte; the gather moves 3/4 of the bytes. */
+#define RM_SHARD_AUTO 0  /* RGB8 once the context gathers (rm_comm_init, ngpus), else RGBA8 */
+#define RM_SHARD_RGBA8 1 /* 4 B per pixel, the display format */
+#define RM_SHARD_RGB8 2  /* 3 B per pixel (sharded contexts only; whole frames stay RGBA8) */
 
 /* ---- shadow modes (rm_uniforms.shadow_mode) ------------------------------- */
 #define RM_SHADOW_SOFT 0 /* reference: softshadow(k = 2.0)  computeShader.glsl:185,236 */
@@ -136,6 +146,12 @@ typedef struct rm_config {
    * balance its render + assembly against the other ranks' render
    * (rm_shard_rows; bench.py --rank0-share). */
   int32_t rank0_rows;
+  /* RM_SHARD_* (API version 6): the layout of this context's RGBA8 shard images
+   * (its own, a caller's rm_set_output_rgba8 buffer, the batch ring, rank 0's
+   * gather buffer) and of the gathered input of rm_unshard_rgba8 /
+   * rm_unshard_batch_rgba8.  rm_read_rgba8 / rm_read_frame_rgba8 of an RGB8 shard
+   * return RGBA8 (alpha 255; the padding rows too).  Ignored unless sharded. */
+  int32_t shard_format;
   /* Multi-GPU frames in one process.  ngpus >= 1 makes the
    * context drive ngpus devices: devices[0..ngpus), or device, device+1, ...
    * when devices is NULL (device -1 = the current device).  Device i renders
@@ -320,9 +336,11 @@ int rm_jit_code_object(const rm_primitive *prims, int32_t n, const char *arch, v
 int rm_set_stream(rm_ctx *ctx, void *hip_stream);
 /* Render RGBA8 into a caller-owned device buffer of >= rows*width*4 bytes
  * (rows = height, or rows_cap when sharded) instead of the context's own.
+ * A sharded context with RGB8 shards writes rows of width*3 bytes there.
  * NULL restores the internal buffer. */
 int rm_set_output_rgba8(rm_ctx *ctx, void *device_ptr);
-/* Device pointer of the RGBA8 image the next dispatch writes. */
+/* Device pointer of the RGBA8 image the next dispatch writes (a shard of an
+ * RGB8 context: packed rows of width*3 bytes, rm_config.shard_format). */
 int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
 /* Orders `hip_stream` (hipStream_t as void*; NULL = the null stream) after every
  * write to the context's images queued so far: work the caller enqueues on it
@@ -335,12 +353,14 @@ int rm_get_output_rgba8(rm_ctx *ctx, void **device_ptr);
 int rm_wait_output(rm_ctx *ctx, void *hip_stream);
 /* Assemble a full image from nshards packed shard images laid out
  * back-to-back ([nshards][rows_cap][width] RGBA8, e.g. the result of an RCCL
- * gather) into `frame` ([height][width] RGBA8), both device pointers, on the
- * context's stream. Uses the context's width/height/row_block/rank0_rows/nshards. */
+ * gather; RGB8, 3 B per pixel, when the context's shard_format is RGB8) into
+ * `frame` ([height][width] RGBA8), both device pointers, on the context's
+ * stream. Uses the context's width/height/row_block/rank0_rows/nshards and
+ * shard format. */
 int rm_unshard_rgba8(rm_ctx *ctx, const void *gathered_dev, void *frame_dev);
 /* The same for frame k of an n-frame batch gathered as rm_dispatch_frames
- * gathers it: [nshards][n][rows_cap][width] RGBA8 (each rank's n shards back to
- * back, ranks in order), e.g. by a host that moves the shards itself. */
+ * gathers it: [nshards][n][rows_cap][width] RGBA8 or RGB8 (each rank's n shards
+ * back to back, ranks in order), e.g. by a host that moves the shards itself. */
 int rm_unshard_batch_rgba8(rm_ctx *ctx, const void *gathered_dev, int32_t k, int32_t n, void *frame_dev);
 /* Kernel timing: when enabled, HIP events bracket every render-kernel launch
  * on the launch stream; rm_kernel_time_ms returns the summed kernel time and
@@ -409,19 +429,21 @@ int rm_comm_rccl_info(rm_ctx *ctx, int32_t *count, int32_t *user_rank, int32_t *
  * ncclGather moves them) is the largest shard's rounds times its rows per round,
  * and *rows is shard s's own count of real rows.  rank0_rows = 0 means
  * row_block (the plain interleave: block b belongs to shard b % nshards).
- * nshards <= 1: the whole image (rows = rows_cap = height). */
+ * nshards <= 1: the whole image (rows = rows_cap = height).
+ * Every function below takes (height, row_block, rank0_rows, nshards, ...) in
+ * this order (API version 6; version 5's rm_shard_row took shard before nshards,
+ * and version 1's rm_shard_rows_cap / rm_shard_global_row knew only the plain
+ * interleave: all three are gone, so a stale caller fails to bind instead of
+ * reading the wrong rows). */
 int rm_shard_rows(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t shard,
                   int32_t *rows, int32_t *rows_cap);
-/* Global row (py) of local row `local_row` of shard `shard`; -1 if padding. */
-int32_t rm_shard_row(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t shard, int32_t nshards,
-                     int32_t local_row);
+/* Global row (py) of local row `local_row` of shard `shard`; -1 if padding or
+ * out of range (including invalid arguments). */
+int32_t rm_shard_to_global(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t shard,
+                           int32_t local_row);
 /* The inverse: the shard and local row that own global row `row`. */
 int rm_shard_owner(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t row,
                    int32_t *shard, int32_t *local_row);
-/* The plain interleave (rank0_rows = row_block), API version 1. */
-int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t *rows_cap);
-int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
-                            int32_t local_row);
 
 /* ---- Camera (source/camera.{hpp,cpp}), glm-free, same formulas ----------- */
 typedef struct rm_camera_state { /* members of camera.hpp:14-27 */

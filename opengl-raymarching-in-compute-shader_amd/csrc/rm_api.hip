@@ -27,7 +27,8 @@ hipError_t launch_table(const rmd::Frame& F, bool counters, hipStream_t s, int n
 hipError_t launch_table_frames(const rmd::FrameBatch& B, int n, hipStream_t s, int nslots, int shape);
 int table_shape(const uint32_t* words, int32_t n);
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0);
+                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows = 0,
+                          bool rgb3 = false);
 hipError_t launch_frames(const rmd::FrameBatch& B, int n, hipStream_t s);
 }  // namespace rm
 static_assert(RM_MAX_BATCH == rmd::kMaxBatch, "rm_api.h RM_MAX_BATCH == rm_scene.hpp kMaxBatch");
@@ -52,6 +53,10 @@ struct rm_ctx {
   bool own_stream = false;
   uint8_t* d_rgba8 = nullptr;     // own RGBA8 image
   uint8_t* ext_rgba8 = nullptr;   // caller-provided RGBA8 image (rm_set_output_rgba8)
+  // the RGBA8 shard images are packed RGB, 3 B per pixel (rm_config.shard_format:
+  // RGB8, or AUTO once the context gathers): the render writes them, the gather
+  // moves them, k_unshard expands them with alpha 255
+  bool rgb3 = false;
   float* d_rgba32f = nullptr;
   uint32_t* d_counts = nullptr;
   unsigned long long* d_counters = nullptr;
@@ -174,6 +179,8 @@ int image_rows(const rm_ctx* c) {
   return c->rows;
 }
 bool full_frame(const rm_ctx* c) { return c->cfg.nshards <= 1 || !c->subs.empty() || comm_root(c); }
+// Bytes per pixel of the context's RGBA8 shard images (rm_config.shard_format).
+size_t bpp8(const rm_ctx* c) { return c->rgb3 ? 3 : 4; }
 // Shard 0's rows per round (rm_config.rank0_rows; 0 = row_block, rm_shard.hpp).
 int row_block0(const rm_ctx* c) { return c->cfg.rank0_rows > 0 ? c->cfg.rank0_rows : c->cfg.row_block; }
 
@@ -549,6 +556,7 @@ rmd::Frame make_frame(const rm_ctx* c) {
   F.nshards = c->cfg.nshards > 1 ? c->cfg.nshards : 1;
   F.rows = c->rows;
   F.rgba8 = render_dst(c);
+  F.rgb3 = c->rgb3 ? 1 : 0;
   F.rgba32f = render_dst32(c);
   F.sdf_counts = c->cfg.counters ? c->d_counts : nullptr;
   F.counters = c->cfg.counters ? c->d_counters : nullptr;
@@ -679,6 +687,8 @@ int comm_attach(rm_ctx* c, ncclComm_t comm, int rank, int n, bool own, bool memb
   c->crank = rank;
   c->cranks = n;
   c->comm_failed = false;
+  // the gathered shards travel as packed RGB unless the config asks for RGBA8
+  if ((c->cfg.outputs & RM_OUT_RGBA8) && c->cfg.shard_format == RM_SHARD_AUTO) c->rgb3 = true;
   if (rank == 0) {
     const size_t px_shard = (size_t)c->rows * c->cfg.width, px_frame = (size_t)c->cfg.height * c->cfg.width;
     if (c->cfg.outputs & RM_OUT_RGBA8) {
@@ -821,7 +831,7 @@ int comm_gather(rm_ctx* c) {
   const bool root = comm_root(c);
   ncclResult_t e = r->GroupStart();
   if (e == ncclSuccess && (c->cfg.outputs & RM_OUT_RGBA8))
-    e = r->Gather(render_dst(c), root ? c->d_gathered : nullptr, px * 4, ncclUint8, 0, c->comm, c->stream);
+    e = r->Gather(render_dst(c), root ? c->d_gathered : nullptr, px * bpp8(c), ncclUint8, 0, c->comm, c->stream);
   if ((e == ncclSuccess || e == ncclInProgress) && (c->cfg.outputs & RM_OUT_RGBA32F))
     e = r->Gather(render_dst32(c), root ? c->d_gathered32 : nullptr, px * 4, ncclFloat32, 0, c->comm,
                   c->stream);
@@ -840,7 +850,8 @@ int comm_assemble(rm_ctx* c) {
   if (!comm_root(c)) return RM_OK;
   if (c->cfg.outputs & RM_OUT_RGBA8) {
     const hipError_t e = rm::launch_unshard(c->d_gathered, image_rgba8(c), c->cfg.width, c->cfg.height,
-                                            c->cfg.row_block, row_block0(c), c->cranks, c->rows, c->stream);
+                                            c->cfg.row_block, row_block0(c), c->cranks, c->rows, c->stream, 0,
+                                            c->rgb3);
     if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   }
   if (c->cfg.outputs & RM_OUT_RGBA32F) {
@@ -909,6 +920,8 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     return fail(nullptr, RM_ERR_INVALID, "rm_create: width/height must be in 1..65536");
   if (cfg->ngpus < 0 || cfg->ngpus > 64)
     return fail(nullptr, RM_ERR_INVALID, "rm_create: ngpus must be in 0..64");
+  if (cfg->shard_format < RM_SHARD_AUTO || cfg->shard_format > RM_SHARD_RGB8)
+    return fail(nullptr, RM_ERR_INVALID, "rm_create: shard_format must be RM_SHARD_AUTO, _RGBA8 or _RGB8");
   if (cfg->ngpus >= 1) {
     if (cfg->kernel < RM_KERNEL_AUTO || cfg->kernel > RM_KERNEL_PIXEL)
       return fail(nullptr, RM_ERR_INVALID, "rm_create: unknown kernel variant");
@@ -936,6 +949,7 @@ int rm_create(rm_ctx** out, const rm_config* cfg) {
     c->cfg.shard = 0;
     if (c->cfg.row_block <= 0) c->cfg.row_block = 1;
   }
+  c->rgb3 = c->cfg.nshards > 1 && c->cfg.shard_format == RM_SHARD_RGB8 && (c->cfg.outputs & RM_OUT_RGBA8);
   if (cfg->device >= 0) {
     c->device = cfg->device;
   } else {
@@ -1355,7 +1369,7 @@ int batch_render(rm_ctx* c, const rm_uniforms* u, int n) {
   if (e0) RM_HIP(c, hipEventRecord(e0, c->stream));
   if ((rc = phase(c, 0)) != RM_OK) return rc;
   rc = launch_batch(
-      c, u, n, [&](int k) { return b.send8 ? b.send8 + (size_t)k * px * 4 : nullptr; },
+      c, u, n, [&](int k) { return b.send8 ? b.send8 + (size_t)k * px * bpp8(c) : nullptr; },
       [&](int k) { return b.send32 ? b.send32 + (size_t)k * px * 4 : nullptr; });
   if (rc != RM_OK) return rc;
   if ((rc = phase(c, 1)) != RM_OK) return rc;
@@ -1373,10 +1387,11 @@ ncclResult_t batch_gather(rm_ctx* c, const rm::Rccl* r, int n) {
   if (set_device(c) != RM_OK) return ncclUnhandledCudaError;
   rm_ctx::BatchSlot& b = c->bslot[c->bnext];
   if (hipStreamWaitEvent(c->gstream, b.rendered, 0) != hipSuccess) return ncclUnhandledCudaError;
-  const size_t count = (size_t)c->rows * (size_t)c->cfg.width * 4 * (size_t)n;  // 4 B or 4 floats per px
+  const size_t px = (size_t)c->rows * (size_t)c->cfg.width * (size_t)n;
+  const size_t count = px * 4;  // 4 floats per px
   const bool root = comm_root(c);
   ncclResult_t e = ncclSuccess;
-  if (b.send8) e = r->Gather(b.send8, root ? b.send8 : nullptr, count, ncclUint8, 0, c->comm, c->gstream);
+  if (b.send8) e = r->Gather(b.send8, root ? b.send8 : nullptr, px * bpp8(c), ncclUint8, 0, c->comm, c->gstream);
   if ((e == ncclSuccess || e == ncclInProgress) && b.send32)
     e = r->Gather(b.send32, root ? b.send32 : nullptr, count, ncclFloat32, 0, c->comm, c->gstream);
   return e;
@@ -1397,8 +1412,8 @@ int batch_finish(rm_ctx* c, int n) {
     for (int k = 0; k < n; ++k) {
       if (b.send8) {
         void* dst = k < n - 1 ? (void*)c->ring8[k] : (void*)image_rgba8(c);
-        const hipError_t e = rm::launch_unshard(b.send8 + (size_t)k * px * 4, dst, W, H, rb, rb0, c->cranks,
-                                                c->rows, c->gstream, stride);
+        const hipError_t e = rm::launch_unshard(b.send8 + (size_t)k * px * bpp8(c), dst, W, H, rb, rb0, c->cranks,
+                                                c->rows, c->gstream, stride, c->rgb3);
         if (e != hipSuccess) return hip_fail(c, e, "unshard launch (batch)");
       }
       if (b.send32) {
@@ -1410,8 +1425,8 @@ int batch_finish(rm_ctx* c, int n) {
     }
   } else {
     if (b.send8 && render_dst(c))
-      RM_HIP(c, hipMemcpyAsync(render_dst(c), b.send8 + (size_t)(n - 1) * px * 4, px * 4, hipMemcpyDeviceToDevice,
-                               c->gstream));
+      RM_HIP(c, hipMemcpyAsync(render_dst(c), b.send8 + (size_t)(n - 1) * px * bpp8(c), px * bpp8(c),
+                               hipMemcpyDeviceToDevice, c->gstream));
     if (b.send32 && render_dst32(c))
       RM_HIP(c, hipMemcpyAsync(render_dst32(c), b.send32 + (size_t)(n - 1) * px * 4, px * 16,
                                hipMemcpyDeviceToDevice, c->gstream));
@@ -1519,8 +1534,10 @@ int rm_synchronize(rm_ctx* c) {
   return stream_wait(c);
 }
 
+// packed3: `dev` is an RGB8 shard image (rows of width x 3 bytes), read back as
+// RGBA8 with alpha 255 (rm_config.shard_format).
 static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t row_pitch,
-                      int flip_y) {
+                      int flip_y, bool packed3 = false) {
   if (!c || !dst) return RM_ERR_INVALID;
   if (!dev) return fail(c, RM_ERR_STATE, "output format not enabled in rm_config.outputs");
   if (!c->dispatched) return fail(c, RM_ERR_STATE, "no dispatch yet");
@@ -1538,6 +1555,22 @@ static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t 
   if (rc != RM_OK) return rc;
   if ((rc = stream_wait(c)) != RM_OK) return rc;
   const size_t rows = (size_t)image_rows(c);
+  if (packed3) {
+    const size_t w3 = (size_t)c->cfg.width * 3;
+    std::vector<uint8_t> tmp(w3 * rows);
+    RM_HIP(c, hipMemcpy(tmp.data(), dev, tmp.size(), hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < rows; ++r) {
+      const uint8_t* s3 = tmp.data() + r * w3;
+      uint8_t* d4 = static_cast<uint8_t*>(dst) + r * row_pitch;
+      for (int x = 0; x < c->cfg.width; ++x) {
+        d4[4 * x] = s3[3 * x];
+        d4[4 * x + 1] = s3[3 * x + 1];
+        d4[4 * x + 2] = s3[3 * x + 2];
+        d4[4 * x + 3] = 255;
+      }
+    }
+    return RM_OK;  // (a shard image: flip_y was refused above)
+  }
   RM_HIP(c, hipMemcpy2D(dst, row_pitch, dev, w, w, rows, hipMemcpyDeviceToHost));
   if (flip_y) {
     // Row 0 of the device image is the bottom row (quad.hpp:9); flip in place
@@ -1557,7 +1590,7 @@ static int read_image(rm_ctx* c, const void* dev, size_t bpp, void* dst, size_t 
 
 int rm_read_rgba8(rm_ctx* c, uint8_t* dst, size_t row_pitch, int flip_y) {
   if (!c) return RM_ERR_INVALID;
-  return read_image(c, image_rgba8(c), 4, dst, row_pitch, flip_y);
+  return read_image(c, image_rgba8(c), 4, dst, row_pitch, flip_y, c->rgb3 && !full_frame(c));
 }
 
 int rm_read_rgba32f(rm_ctx* c, float* dst, size_t row_pitch, int flip_y) {
@@ -1580,12 +1613,12 @@ static int read_frame(rm_ctx* c, int32_t k, bool f32, void* dst, size_t row_pitc
     const rm_ctx::BatchSlot& b = t->bslot[t->blast];
     const size_t px = (size_t)t->rows * (size_t)t->cfg.width;
     dev = f32 ? (const void*)(b.send32 ? b.send32 + (size_t)k * px * 4 : nullptr)
-              : (const void*)(b.send8 ? b.send8 + (size_t)k * px * 4 : nullptr);
+              : (const void*)(b.send8 ? b.send8 + (size_t)k * px * bpp8(t) : nullptr);
   } else {
     dev = f32 ? (const void*)((size_t)k < t->ring32.size() ? t->ring32[k] : nullptr)
               : (const void*)((size_t)k < t->ring8.size() ? t->ring8[k] : nullptr);
   }
-  return read_image(c, dev, f32 ? 16 : 4, dst, row_pitch, flip_y);
+  return read_image(c, dev, f32 ? 16 : 4, dst, row_pitch, flip_y, !f32 && t->rgb3 && !full_frame(t));
 }
 
 int rm_read_frame_rgba8(rm_ctx* c, int32_t k, uint8_t* dst, size_t row_pitch, int flip_y) {
@@ -1913,7 +1946,8 @@ int rm_unshard_rgba8(rm_ctx* c, const void* gathered_dev, void* frame_dev) {
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   hipError_t e = rm::launch_unshard(gathered_dev, frame_dev, c->cfg.width, c->cfg.height,
-                                    c->cfg.row_block, row_block0(c), c->cfg.nshards, c->rows, c->stream);
+                                    c->cfg.row_block, row_block0(c), c->cfg.nshards, c->rows, c->stream, 0,
+                                    c->rgb3);
   if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }
@@ -1925,9 +1959,10 @@ int rm_unshard_batch_rgba8(rm_ctx* c, const void* gathered_dev, int32_t k, int32
   int rc = set_device(c);
   if (rc != RM_OK) return rc;
   const size_t px = (size_t)c->rows * (size_t)c->cfg.width;
-  const uint8_t* src = static_cast<const uint8_t*>(gathered_dev) + (size_t)k * px * 4;
+  const uint8_t* src = static_cast<const uint8_t*>(gathered_dev) + (size_t)k * px * bpp8(c);
   hipError_t e = rm::launch_unshard(src, frame_dev, c->cfg.width, c->cfg.height, c->cfg.row_block,
-                                    row_block0(c), c->cfg.nshards, c->rows, c->stream, (size_t)n * (size_t)c->rows);
+                                    row_block0(c), c->cfg.nshards, c->rows, c->stream, (size_t)n * (size_t)c->rows,
+                                    c->rgb3);
   if (e != hipSuccess) return hip_fail(c, e, "unshard launch");
   return RM_OK;
 }
@@ -1978,6 +2013,44 @@ int rm_comm_unique_id(void* id, size_t size) {
   return RM_OK;
 }
 
+namespace {
+//  Every rank of a communicator must cut the frame the same way, or
+// the gather's counts differ (a stall until the deadline) or k_unshard puts rows
+// in the wrong places: the ranks exchange (width, height, row_block, rank 0's
+// rows per round, outputs, shard format) with one ncclAllGather on the new
+// communicator, and a rank that sees a difference aborts it (every rank sees the
+// same table, so every rank fails the same way) with RM_ERR_INVALID.
+int comm_check_layout(rm_ctx* c, const rm::Rccl* r) {
+  constexpr int K = 6;
+  const int32_t mine[K] = {c->cfg.width, c->cfg.height, c->cfg.row_block, row_block0(c), c->cfg.outputs,
+                           c->rgb3 ? RM_SHARD_RGB8 : RM_SHARD_RGBA8};
+  int32_t* d = nullptr;
+  RM_HIP(c, hipMalloc(&d, sizeof(mine) * (size_t)c->cranks));
+  std::vector<int32_t> all((size_t)K * c->cranks, 0);
+  hipError_t he = hipMemcpyAsync(d + (size_t)K * c->crank, mine, sizeof mine, hipMemcpyHostToDevice, c->stream);
+  ncclResult_t e = ncclSuccess;
+  if (he == hipSuccess) e = r->AllGather(d + (size_t)K * c->crank, d, K, ncclInt32, c->comm, c->stream);
+  int rc = he != hipSuccess ? hip_fail(c, he, "hipMemcpyAsync (layout)")
+                            : comm_enqueued(c, r, e, "ncclAllGather (rm_comm_init layout check)");
+  if (rc == RM_OK) rc = comm_wait(c);  // bounded: a rank that dies here is RM_ERR_COMM
+  if (rc == RM_OK && (he = hipMemcpy(all.data(), d, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+    rc = hip_fail(c, he, "hipMemcpy (layout)");
+  (void)hipFree(d);
+  if (rc != RM_OK) return rc;
+  static const char* names[K] = {"width", "height", "row_block", "rank0_rows", "outputs", "shard_format"};
+  for (int q = 0; q < c->cranks; ++q)
+    for (int k = 0; k < K; ++k)
+      if (all[(size_t)K * q + k] != all[k]) {
+        const std::string why = std::string("rm_comm_init: ranks 0 and ") + std::to_string(q) + " disagree on " +
+                                names[k] + " (" + std::to_string(all[k]) + " vs " +
+                                std::to_string(all[(size_t)K * q + k]) + "): every rank must shard the frame alike";
+        (void)comm_abort(c, why);
+        return fail(c, RM_ERR_INVALID, why);
+      }
+  return RM_OK;
+}
+}  // namespace
+
 int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
   if (!c || !id) return RM_ERR_INVALID;
   if (!c->subs.empty()) return fail(c, RM_ERR_STATE, "a multi-GPU context has its own communicator");
@@ -2019,7 +2092,7 @@ int rm_comm_init(rm_ctx* c, const void* id, int32_t nranks, int32_t rank) {
     c->comm = nullptr;
     return rc;
   }
-  return RM_OK;
+  return comm_check_layout(c, r);
 }
 
 int rm_comm_set_timeout(rm_ctx* c, int32_t timeout_ms) {

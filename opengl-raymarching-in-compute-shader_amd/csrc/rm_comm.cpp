@@ -48,6 +48,7 @@ void load() {
   sym("ncclGroupStart", g_rccl.GroupStart);
   sym("ncclGroupEnd", g_rccl.GroupEnd);
   sym("ncclGather", g_rccl.Gather);
+  sym("ncclAllGather", g_rccl.AllGather);
   sym("ncclGetErrorString", g_rccl.GetErrorString);
   sym("ncclGetVersion", g_rccl.GetVersion);
   sym("ncclCommCount", g_rccl.CommCount);

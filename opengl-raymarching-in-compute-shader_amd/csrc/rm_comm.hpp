@@ -25,6 +25,7 @@ struct Rccl {
   decltype(&ncclGroupStart) GroupStart;
   decltype(&ncclGroupEnd) GroupEnd;
   decltype(&ncclGather) Gather;
+  decltype(&ncclAllGather) AllGather;  // rm_comm_init's check that every rank cuts the frame alike
   decltype(&ncclGetErrorString) GetErrorString;
   decltype(&ncclGetVersion) GetVersion;
   // what the communicator itself reports (rm_comm_rccl_info): the rank count and

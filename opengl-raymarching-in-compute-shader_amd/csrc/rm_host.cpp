@@ -375,8 +375,8 @@ int rm_shard_rows(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t
   return RM_OK;
 }
 
-int32_t rm_shard_row(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t shard, int32_t nshards,
-                     int32_t local_row) {
+int32_t rm_shard_to_global(int32_t height, int32_t row_block, int32_t rank0_rows, int32_t nshards, int32_t shard,
+                           int32_t local_row) {
   if (local_row < 0 || height <= 0 || height > 65536) return -1;
   if (nshards <= 1) return (shard == 0 && local_row < height) ? local_row : -1;
   rm::ShardMap m;
@@ -398,16 +398,6 @@ int rm_shard_owner(int32_t height, int32_t row_block, int32_t rank0_rows, int32_
   if (!shard_map(row_block, rank0_rows, nshards, &m)) return RM_ERR_INVALID;
   rm::shard_owner(m, row, shard, local_row);
   return RM_OK;
-}
-
-int rm_shard_rows_cap(int32_t height, int32_t row_block, int32_t nshards, int32_t* rows_cap) {
-  if (!rows_cap) return RM_ERR_INVALID;
-  return rm_shard_rows(height, row_block, row_block, nshards, 0, nullptr, rows_cap);
-}
-
-int32_t rm_shard_global_row(int32_t height, int32_t row_block, int32_t shard, int32_t nshards,
-                            int32_t local_row) {
-  return rm_shard_row(height, row_block, row_block, shard, nshards, local_row);
 }
 
 }  // extern "C"

@@ -598,7 +598,11 @@ __global__ __launch_bounds__(64, 8) void k_sample_frames(FrameBatch B) {
 // row; rm_shard.hpp's weighted interleave) is computed once per workgroup in
 // scalar registers; lanes copy 16 B (4 pixels) each when rows are 16-B aligned
 // (width % 4 == 0 and both images 16-B aligned), one pixel otherwise.
-template <bool VEC>
+// RGB3: the shards are packed RGB (3 B per pixel, rm_config.shard_format): a
+// lane reads a group of 4 pixels as 3 dwords (rows of 3 width bytes are 4-B
+// aligned when width % 4 == 0) and writes them as RGBA with alpha 255, the
+// reference's constant alpha 1.0 quantised.
+template <bool VEC, bool RGB3>
 __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ gathered,
                                                  uint32_t* __restrict__ frame, int width,
                                                  int height, rm::ShardMap map,
@@ -607,8 +611,26 @@ __global__ __launch_bounds__(256) void k_unshard(const uint32_t* __restrict__ ga
   for (int y = blockIdx.y; y < height; y += gridDim.y) {  // gridDim.y <= 65535
     int r, lrow;
     rm::shard_owner(map, y, &r, &lrow);
-    const uint32_t* src = gathered + ((size_t)r * rank_stride + lrow) * (size_t)width;
+    const size_t srow = (size_t)r * rank_stride + lrow;
     uint32_t* dst = frame + (size_t)y * (size_t)width;
+    if (RGB3) {
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(gathered) + srow * (size_t)width * 3;
+      if (VEC) {
+        const int nw = width / 4, lanes = (int)(gridDim.x * blockDim.x);
+        for (int j = i; j < nw && j < i + 2 * lanes; j += lanes) {
+          const uint32_t* s3 = reinterpret_cast<const uint32_t*>(src) + 3 * (size_t)j;
+          const uint32_t a = s3[0], b = s3[1], c = s3[2];
+          reinterpret_cast<uint4*>(dst)[j] =
+              make_uint4(a | 0xff000000u, (a >> 24) | (b << 8) | 0xff000000u,
+                         (b >> 16) | (c << 16) | 0xff000000u, (c >> 8) | 0xff000000u);
+        }
+      } else if (i < width) {
+        const uint8_t* p = src + 3 * (size_t)i;
+        dst[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | 0xff000000u;
+      }
+      continue;
+    }
+    const uint32_t* src = gathered + srow * (size_t)width;
     if (VEC) {
       // two 16-byte words per lane, the lanes of a row strided (round 4,
       // tools/probe_unshard.py: 10.4 against 11.0 us per 4K frame, 6.4 TB/s;
@@ -695,22 +717,29 @@ hipError_t debug_stats(unsigned long long* out, bool clear) {
 
 #ifndef RM_KERNELS_AA_ONLY
 hipError_t launch_unshard(const void* gathered, void* frame, int width, int height, int row_block,
-                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows) {
+                          int row_block0, int nshards, int rows_cap, hipStream_t s, size_t rank_stride_rows,
+                          bool rgb3) {
   if (nshards < 1 || row_block < 1 || row_block0 < 1) return hipErrorInvalidValue;
   const rm::ShardMap map{row_block, row_block0, nshards};
   const size_t stride = rank_stride_rows ? rank_stride_rows : (size_t)rows_cap;
   // 16-B copies need 16-B rows (width % 4 == 0) and 16-B aligned images: the
-  // C-ABI takes caller pointers, which may be offset
-  const bool vec = width % 4 == 0 && ((reinterpret_cast<uintptr_t>(gathered) |
-                                       reinterpret_cast<uintptr_t>(frame)) % 16 == 0);
+  // C-ABI takes caller pointers, which may be offset (packed RGB sources: 4-B)
+  const uintptr_t ga = reinterpret_cast<uintptr_t>(gathered), fa = reinterpret_cast<uintptr_t>(frame);
+  const bool vec = width % 4 == 0 && fa % 16 == 0 && ga % (rgb3 ? 4 : 16) == 0;
   const unsigned per_row = (unsigned)(vec ? (width / 4 + 1) / 2 : width);  // lanes per row
   const dim3 grid((per_row + 255) / 256, (unsigned)(height < 65535 ? height : 65535));
   const uint32_t* g = static_cast<const uint32_t*>(gathered);
   uint32_t* f = static_cast<uint32_t*>(frame);
-  if (vec)
-    hipLaunchKernelGGL(rmd::k_unshard<true>, grid, dim3(256), 0, s, g, f, width, height, map, stride);
-  else
-    hipLaunchKernelGGL(rmd::k_unshard<false>, grid, dim3(256), 0, s, g, f, width, height, map, stride);
+  if (rgb3) {
+    if (vec)
+      hipLaunchKernelGGL((rmd::k_unshard<true, true>), grid, dim3(256), 0, s, g, f, width, height, map, stride);
+    else
+      hipLaunchKernelGGL((rmd::k_unshard<false, true>), grid, dim3(256), 0, s, g, f, width, height, map, stride);
+  } else if (vec) {
+    hipLaunchKernelGGL((rmd::k_unshard<true, false>), grid, dim3(256), 0, s, g, f, width, height, map, stride);
+  } else {
+    hipLaunchKernelGGL((rmd::k_unshard<false, false>), grid, dim3(256), 0, s, g, f, width, height, map, stride);
+  }
   return hipGetLastError();
 }
 #endif

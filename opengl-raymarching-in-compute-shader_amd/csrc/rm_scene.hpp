@@ -109,6 +109,9 @@ struct Frame {
   int32_t nprims;        // entries in `scene`
   int32_t grid_x, grid_y;  // k_pixel / k_sample grid (rm::pixel_grid): ordinary kernel
                            // arguments, loaded with the rest of the prologue's
+  int32_t rgb3;  // rgba8 holds a packed RGB shard, [rows][width][3] (rm_config.shard_format):
+                 // the alpha the reference stores is the constant 1.0 (glsl:314-341), so a
+                 // gathered shard carries 3 B per pixel and the un-shard writes alpha 255
 };
 
 // A batch of frames of one context (rm_dispatch_frames): one grid over n frames
@@ -982,8 +985,15 @@ __device__ __forceinline__ int global_row(const Frame& F, int local_row) {
 __device__ __forceinline__ void store_pixel(const Frame& F, size_t idx, float r, float g, float b,
                                             float a) {
   if (F.rgba8) {
-    uint32_t w = quantize(r) | (quantize(g) << 8) | (quantize(b) << 16) | (quantize(a) << 24);
-    reinterpret_cast<uint32_t*>(F.rgba8)[idx] = w;
+    if (F.rgb3) {  // uniform: a scalar branch
+      uint8_t* p = F.rgba8 + idx * 3;
+      p[0] = (uint8_t)quantize(r);
+      p[1] = (uint8_t)quantize(g);
+      p[2] = (uint8_t)quantize(b);
+    } else {
+      uint32_t w = quantize(r) | (quantize(g) << 8) | (quantize(b) << 16) | (quantize(a) << 24);
+      reinterpret_cast<uint32_t*>(F.rgba8)[idx] = w;
+    }
   }
   if (F.rgba32f) reinterpret_cast<float4*>(F.rgba32f)[idx] = make_float4(r, g, b, a);
 }

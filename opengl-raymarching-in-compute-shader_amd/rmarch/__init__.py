@@ -32,8 +32,8 @@ RM_ERR_NO_DEVICE = -4
 RM_ERR_STATE = -5
 RM_ERR_COMM = -6
 
-RM_API_VERSION = 5
-RM_CONFIG_MAGIC = 0x35434D52
+RM_API_VERSION = 6
+RM_CONFIG_MAGIC = 0x36434D52
 
 RM_MAX_BATCH = 32
 RM_OUT_RGBA8 = 1
@@ -42,6 +42,9 @@ RM_SHADOW_SOFT = 0
 RM_SHADOW_HARD = 1
 RM_KERNEL_AUTO = 0
 RM_KERNEL_PIXEL = 1
+RM_SHARD_AUTO = 0   # RGB8 shards once the context gathers, RGBA8 otherwise (rm_config.shard_format)
+RM_SHARD_RGBA8 = 1
+RM_SHARD_RGB8 = 2
 
 
 class RMError(RuntimeError):
@@ -82,7 +85,8 @@ class rm_config(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("magic", C.c_uint32), ("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32),
                 ("outputs", C.c_int32), ("kernel", C.c_int32), ("counters", C.c_int32),
                 ("row_block", C.c_int32), ("shard", C.c_int32), ("nshards", C.c_int32),
-                ("rank0_rows", C.c_int32), ("ngpus", C.c_int32), ("devices", C.POINTER(C.c_int32))]
+                ("rank0_rows", C.c_int32), ("shard_format", C.c_int32), ("ngpus", C.c_int32),
+                ("devices", C.POINTER(C.c_int32))]
 
 
 class rm_camera_state(C.Structure):
@@ -198,11 +202,9 @@ _SIGS = {
                                   C.POINTER(C.c_double)]),
     "rm_shard_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
-    "rm_shard_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rm_shard_to_global": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rm_shard_owner": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
-    "rm_shard_rows_cap": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
-    "rm_shard_global_row": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rm_camera_init": (C.c_int, [C.POINTER(rm_camera_state), C.c_int32, C.c_int32, C.c_float,
                                  C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                  C.POINTER(C.c_float)]),
@@ -411,17 +413,20 @@ class Renderer:
     def __init__(self, width: int, height: int, *, outputs: int = RM_OUT_RGBA8,
                  kernel: int = RM_KERNEL_AUTO, counters: bool = False, device: int = -1,
                  row_block: int = 0, shard: int = 0, nshards: int = 1, ngpus: int = 0,
-                 devices: Optional[Sequence[int]] = None, rank0_rows: int = 0):
+                 devices: Optional[Sequence[int]] = None, rank0_rows: int = 0,
+                 shard_format: int = RM_SHARD_AUTO):
         """ngpus >= 1: one context over ngpus devices (`devices`, or device,
         device+1, ...), shards gathered with RCCL on the first (rm_config.ngpus).
-        rank0_rows: shard 0's rows per round of the weighted interleave (0 = row_block)."""
+        rank0_rows: shard 0's rows per round of the weighted interleave (0 = row_block).
+        shard_format: RM_SHARD_* layout of the RGBA8 shard images (AUTO: packed RGB
+        once the context gathers)."""
         devs = (C.c_int32 * len(devices))(*devices) if devices else None
         if devices:
             ngpus = len(devices)
         cfg = rm_config(struct_size=C.sizeof(rm_config), magic=RM_CONFIG_MAGIC, width=width, height=height,
                         device=device, outputs=outputs, kernel=kernel,
                         counters=1 if counters else 0, row_block=row_block, shard=shard,
-                        nshards=nshards, rank0_rows=rank0_rows, ngpus=ngpus,
+                        nshards=nshards, rank0_rows=rank0_rows, shard_format=shard_format, ngpus=ngpus,
                         devices=C.cast(devs, C.POINTER(C.c_int32)) if devs else None)
         h = C.c_void_p()
         _check(lib().rm_create(C.byref(h), C.byref(cfg)))
@@ -430,6 +435,7 @@ class Renderer:
         self.outputs = outputs if outputs else RM_OUT_RGBA8
         self.nshards, self.shard, self.row_block = max(nshards, 1), shard, row_block
         self.rank0_rows = rank0_rows
+        self.shard_format = shard_format
         self.ngpus = ngpus
         self.rows = (shard_rows(height, row_block, nshards, shard, rank0_rows)[1]
                      if nshards > 1 and not ngpus else height)
@@ -697,9 +703,9 @@ def shard_rows_cap(height: int, row_block: int, nshards: int, rank0_rows: int = 
 
 def shard_global_rows(height: int, row_block: int, shard: int, nshards: int,
                       rank0_rows: int = 0) -> np.ndarray:
-    """Global row of every local row of `shard` (-1: padding), rm_shard_row."""
+    """Global row of every local row of `shard` (-1: padding), rm_shard_to_global."""
     cap = shard_rows_cap(height, row_block, nshards, rank0_rows)
-    return np.array([lib().rm_shard_row(height, row_block, rank0_rows, shard, nshards, r)
+    return np.array([lib().rm_shard_to_global(height, row_block, rank0_rows, nshards, shard, r)
                      for r in range(cap)], np.int32)
 
 

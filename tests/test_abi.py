@@ -44,7 +44,7 @@ def test_structs_match_header_sizes(rm):
     assert C.sizeof(rm.rm_light) == 60
     assert C.sizeof(rm.rm_uniforms) == 64 + 60 + 4 * 5 + 12 + 8 + 4
     assert C.sizeof(rm.rm_counters) == 56
-    assert C.sizeof(rm.rm_config) == 64  # struct_size + magic + 11 int32 + pad + the devices pointer
+    assert C.sizeof(rm.rm_config) == 64  # struct_size + magic + 12 int32 + the devices pointer
     assert C.sizeof(rm.rm_camera_state) == 8 + 24 + 48
 
 
@@ -74,7 +74,7 @@ def test_struct_layouts_match_the_c_compiler(rm, tmp_path):
 
 
 def test_api_version(rm):
-    assert rm.lib().rm_api_version() == 5 == rm.RM_API_VERSION
+    assert rm.lib().rm_api_version() == 6 == rm.RM_API_VERSION
 
 
 def test_config_struct_size_is_checked(rm):
@@ -103,6 +103,65 @@ def test_config_struct_size_is_checked(rm):
     assert rm.lib().rm_create(C.byref(h), C.byref(v4)) == rm.RM_ERR_INVALID
     assert b"magic" in rm.lib().rm_last_error(None)
     assert not h.value
+    # a v5 host (magic "RMC5"): the same 64 bytes as v6, whose shard_format sits where
+    # v5 had ngpus: refused by the magic
+    v5 = rm.rm_config(struct_size=C.sizeof(rm.rm_config), magic=0x35434D52, width=64, height=32)
+    assert rm.lib().rm_create(C.byref(h), C.byref(v5)) == rm.RM_ERR_INVALID
+    assert b"magic" in rm.lib().rm_last_error(None)
+    assert not h.value
+
+
+def test_shard_format_validation_without_gpu(rm):
+    """rm_config.shard_format (API version 6) outside RM_SHARD_* is refused before any
+    device call, for one-device and multi-GPU contexts alike."""
+    for kw in (dict(nshards=2, row_block=8), dict(ngpus=2)):
+        for bad in (-1, 3):
+            with pytest.raises(rm.RMError) as e:
+                rm.Renderer(64, 64, shard_format=bad, **kw)
+            assert e.value.code == rm.RM_ERR_INVALID and "shard_format" in str(e.value)
+
+
+def _model_owner(H, R, R0, N):
+    """Independent model of the weighted interleave: the owner shard and local row
+    of every global row, walking the rounds."""
+    own, loc, cnt = [], [], [0] * N
+    while len(own) < H:
+        for s in range(N):
+            for _ in range(R0 if s == 0 else R):
+                own.append(s)
+                loc.append(cnt[s])
+                cnt[s] += 1
+    return own[:H], loc[:H]
+
+
+@pytest.mark.parametrize("H,R,R0,N", [(2160, 8, 7, 8), (2160, 8, 0, 4), (541, 3, 2, 5), (64, 8, 13, 2),
+                                      (17, 4, 1, 3), (100, 8, 8, 1)])
+def test_every_shard_function_against_the_model(rm, H, R, R0, N):
+    """every shard function of the C-ABI, called directly with a
+    weighted map, agrees with the pure model; all take (height, row_block,
+    rank0_rows, nshards, ...) in that order (API version 6)."""
+    L = rm.lib()
+    r0 = R0 or R
+    own, loc = _model_owner(H, R, r0, max(N, 1))
+    n, cap = C.c_int32(0), C.c_int32(0)
+    caps = set()
+    for s in range(N):
+        assert L.rm_shard_rows(H, R, R0, N, s, C.byref(n), C.byref(cap)) == rm.RM_OK
+        caps.add(cap.value)
+        mine = [y for y in range(H) if own[y] == s]
+        assert n.value == len(mine)
+        for j, y in enumerate(mine):
+            assert L.rm_shard_to_global(H, R, R0, N, s, j) == y
+        for j in range(len(mine), cap.value):
+            assert L.rm_shard_to_global(H, R, R0, N, s, j) == -1
+    assert len(caps) == 1, "every shard image has the same rows_cap"
+    for y in range(H):
+        s_, l_ = C.c_int32(-1), C.c_int32(-1)
+        assert L.rm_shard_owner(H, R, R0, N, y, C.byref(s_), C.byref(l_)) == rm.RM_OK
+        assert (s_.value, l_.value) == (own[y], loc[y])
+    # the v5 signature's order (shard before nshards) no longer binds
+    assert not hasattr(L, "rm_shard_row") and not hasattr(L, "rm_shard_rows_cap")
+    assert not hasattr(L, "rm_shard_global_row")
 
 
 def test_multi_gpu_config_validation_without_gpu(rm):

@@ -26,6 +26,36 @@ def test_default_batches():
     assert b.default_batch(3, False, False, 30) == 2
     assert b.default_batch(4, False, False, 20) == 2
     assert b.default_batch(5, False, False, 20) == 1
-    # N > 1: single frames in flight, or batches of 4 on one communicator
-    assert b.default_batch(3, True, False, 30) == 1
+    # N > 1: pairs of frames per launch (round 6, tools/probe_scale.py), or batches
+    # of 4 on one communicator
+    assert b.default_batch(3, True, False, 30) == 2
     assert b.default_batch(3, True, True, 30) == 4
+
+
+def test_run_mode_selection():
+    """--gpus N > 1 without a launcher runs in this one process over
+    N devices (rm_config.ngpus); a launcher's world size must equal N."""
+    b = _bench()
+    assert b.run_mode(1, False, 1, False) == ("single_gpu", None)
+    assert b.run_mode(8, False, 1, False) == ("single_process", None)
+    assert b.run_mode(1, False, 1, True) == ("single_process", None)
+    assert b.run_mode(8, True, 8, False) == ("launcher", None)
+    assert b.run_mode(1, True, 1, False) == ("launcher", None)
+    mode, why = b.run_mode(8, True, 4, False)
+    assert mode == "error" and "WORLD_SIZE=4" in why
+    assert b.run_mode(2, True, 2, True)[0] == "error"
+    assert b.run_mode(0, False, 1, False)[0] == "error"
+
+
+def test_gpus_beyond_the_visible_devices_exits_2():
+    """--gpus N in one process with fewer than N visible devices: a clear message
+    and status 2, before any context is created (here: no GPU at all)."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = env.get("HIP_VISIBLE_DEVICES", "")  # (no change on a box)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64", "--steps", "2"],
+                         env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 2, (out.returncode, out.stderr[-2000:])
+    assert "--gpus 64 in one process needs 64 visible devices" in out.stderr
+    assert out.stdout.strip() == ""

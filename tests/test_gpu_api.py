@@ -139,19 +139,24 @@ def test_kernel_timing(rm, gpu):
 @pytest.mark.parametrize("N,R,R0", [(2, 8, 8), (3, 4, 4), (8, 8, 8), (2, 8, 7), (4, 8, 5), (8, 8, 7),
                                     (3, 4, 9)])
 @pytest.mark.parametrize("W", [80, 83])  # 16-B row copies / per-pixel copies in k_unshard
-def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, R0, W):
+@pytest.mark.parametrize("fmt", ["rgba8", "rgb8"])
+def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, R0, W, fmt):
     """Virtual ranks of the (weighted) interleave: every shard
     rendered into its slot of one gather buffer and assembled by k_unshard equals
-    the full render byte for byte."""
+    the full render byte for byte; also with packed RGB shards (API version 6,
+    rm_config.shard_format: 3 B per pixel, alpha 255 restored by the un-shard)."""
     import torch
     H = 61
     k = rm.RM_KERNEL_PIXEL
     u = rm.sweep_uniforms(70, 120, 3, aa, 0)
     full = render(rm, u, W, H, kernel=k)
     cap = rm.shard_rows_cap(H, R, N, R0)
-    gathered = torch.zeros((N, cap, W, 4), dtype=torch.uint8, device="cuda")
+    bpp = 3 if fmt == "rgb8" else 4
+    sf = rm.RM_SHARD_RGB8 if fmt == "rgb8" else rm.RM_SHARD_RGBA8
+    gathered = torch.zeros((N, cap, W, bpp), dtype=torch.uint8, device="cuda")
     frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-    rs = [rm.Renderer(W, H, kernel=k, row_block=R, shard=i, nshards=N, rank0_rows=R0) for i in range(N)]
+    rs = [rm.Renderer(W, H, kernel=k, row_block=R, shard=i, nshards=N, rank0_rows=R0, shard_format=sf)
+          for i in range(N)]
     for i, r in enumerate(rs):
         r.set_output_rgba8(gathered[i].data_ptr())
         r.dispatch(u)
@@ -161,6 +166,39 @@ def test_shards_assemble_to_the_full_frame(rm, gpu, aa, N, R, R0, W):
     np.testing.assert_array_equal(frame.cpu().numpy(), full)
     for r in rs:
         r.close()
+
+
+@pytest.mark.parametrize("aa", [True, False], ids=["k_sample", "k_pixel"])
+def test_rgb8_shard_is_the_rgba8_shard_without_alpha(rm, gpu, aa):
+    """An RGB8 shard image (rm_config.shard_format, API version 6) holds exactly the
+    R, G, B bytes of the RGBA8 shard, packed; its readback (rm_read_rgba8) expands
+    it with alpha 255, which is every real pixel's alpha (the reference's constant
+    1.0); a bad shard_format is refused."""
+    import torch
+    W, H, N, R, R0 = 37, 29, 3, 4, 3
+    u = rm.sweep_uniforms(55, 120, 2, aa, 0)
+    for s in range(N):
+        rows = rm.shard_global_rows(H, R, s, N, R0)
+        real = rows >= 0
+        with rm.Renderer(W, H, row_block=R, shard=s, nshards=N, rank0_rows=R0,
+                         shard_format=rm.RM_SHARD_RGBA8) as a, \
+             rm.Renderer(W, H, row_block=R, shard=s, nshards=N, rank0_rows=R0,
+                         shard_format=rm.RM_SHARD_RGB8) as b:
+            a.dispatch(u)
+            b.dispatch(u)
+            ia, ib = a.read_rgba8(), b.read_rgba8()
+            np.testing.assert_array_equal(ib[real], ia[real])
+            assert (ia[real][..., 3] == 255).all() and (ib[..., 3] == 255).all()
+            # the device bytes: packed rows of 3 x width
+            dev = torch.zeros(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
+            b.set_output_rgba8(dev.data_ptr())
+            b.dispatch(u)
+            b.synchronize()
+            packed = dev.cpu().numpy().reshape(len(rows), W, 3)
+            np.testing.assert_array_equal(packed[real], ia[real][..., :3])
+    with pytest.raises(rm.RMError) as e:
+        rm.Renderer(W, H, row_block=R, shard=0, nshards=N, shard_format=7)
+    assert e.value.code == rm.RM_ERR_INVALID
 
 
 # ---- full-size properties (oracle too slow at these sizes) ----------------------------

@@ -338,25 +338,30 @@ def test_batch_full_size(rm, gpu, cfg):
 
 
 @pytest.mark.parametrize("N,R,R0,n", [(2, 8, 8, 5), (3, 4, 4, 3), (8, 8, 8, 4), (8, 8, 7, 4), (4, 8, 6, 3)])
-def test_batch_gather_layout_assembles(rm, gpu, N, R, R0, n):
+@pytest.mark.parametrize("fmt", ["rgba8", "rgb8"])
+def test_batch_gather_layout_assembles(rm, gpu, N, R, R0, n, fmt):
     """The N-rank layout of a gathered batch, rehearsed with N virtual ranks on one GPU
     (RCCL refuses two ranks on one device): rank r's n shards rendered by
     rm_dispatch_frames, placed as ncclGather places them on rank 0 ([N][n][rows_cap]
     [width]: each rank's n shards back to back), and every frame k assembled by
     rm_unshard_batch_rgba8 (the k_unshard launch rm_dispatch_frames uses on rank 0,
-    rank stride n x rows_cap) equals a full render."""
+    rank stride n x rows_cap) equals a full render.  fmt rgb8: the shards are packed
+    RGB (rm_config.shard_format, API version 6), as a communicator context gathers
+    them: rendered packed, read back expanded, packed again for the gather buffer."""
     import torch
     W, H = 160, 90
     us = _frames(rm, n)
     cap = rm.shard_rows_cap(H, R, N, R0)
-    gathered = torch.zeros((N, n, cap, W, 4), dtype=torch.uint8, device="cuda")
+    sf = rm.RM_SHARD_RGB8 if fmt == "rgb8" else rm.RM_SHARD_RGBA8
+    bpp = 3 if fmt == "rgb8" else 4
+    gathered = torch.zeros((N, n, cap, W, bpp), dtype=torch.uint8, device="cuda")
     for r in range(N):
-        with rm.Renderer(W, H, row_block=R, shard=r, nshards=N, rank0_rows=R0) as s:
+        with rm.Renderer(W, H, row_block=R, shard=r, nshards=N, rank0_rows=R0, shard_format=sf) as s:
             s.dispatch_frames(us)
             for k in range(n):
-                gathered[r, k] = torch.from_numpy(s.read_frame_rgba8(k)).cuda()
+                gathered[r, k] = torch.from_numpy(s.read_frame_rgba8(k)[..., :bpp].copy()).cuda()
     ref = _per_frame(rm, W, H, us, outputs=rm.RM_OUT_RGBA8)
-    with rm.Renderer(W, H, row_block=R, shard=0, nshards=N, rank0_rows=R0) as a:
+    with rm.Renderer(W, H, row_block=R, shard=0, nshards=N, rank0_rows=R0, shard_format=sf) as a:
         for k in range(n):
             frame = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
             torch.cuda.synchronize()

@@ -62,8 +62,38 @@ def test_bench_rccl_path_at_world_size_one(args):
     assert rc["nranks_seen"] == [1] and rc["all_communicators_match"] and rc["version"] > 0, rc
     ncomm = d["config"]["communicators_per_rank"]
     one = "--comms" in args or ("--pipeline" in args and args[args.index("--pipeline") + 1] == "0")
-    assert len(rc["per_rank"][0]["comms"]) == ncomm == (1 if one else 4), rc
+    assert len(rc["per_rank"][0]["comms"]) == ncomm == (1 if one else 2), rc
     assert "render kernel" in d["roofline"]["kernel_time_basis"] or args[-1] == "0"
+    assert d["config"]["shard_format"].startswith("RGB8") and d["config"]["rank0_rows_source"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ("--config", "2", "--steps", "6", "--warmup", "2"),
+    ("--config", "3", "--steps", "4", "--warmup", "2", "--batch", "1"),
+])
+def test_bench_single_process_ngpus_path(args):
+    """`python bench.py --gpus N` without a launcher runs the sharded,
+    RCCL-gathered step in one process over N devices (rm_config.ngpus contexts: one
+    shard per device, a single-process communicator, grouped gather, assembly on
+    device 0).  --single-process forces that path at N = 1, so one GPU runs it: the
+    same JSON line, RCCL's own view of every communicator, per-phase times and the
+    assembled frame equal to a plain one-GPU render."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                             "RM_BENCH_FORCE_DIST")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--single-process",
+                          *args], env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = out.stdout.strip().splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and "one process (rm_config.ngpus)" in d["config"]["parallelism"]
+    assert d["parity"]["assembled_equals_single_gpu"] and d["parity"]["max_abs_delta_rgba8"] == 0
+    rc = d["rccl"]
+    assert rc["nranks_seen"] == [1] and rc["all_communicators_match"] and rc["version"] > 0, rc
+    ph = d["phases"]
+    assert ph["frames"] == int(args[args.index("--steps") + 1]) and ph["max_render_mean_ms"] > 0, ph
+    assert d["value"] > 0 and d["cpu_baseline"] is None
 
 
 @pytest.mark.gpu

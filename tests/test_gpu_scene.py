@@ -184,7 +184,7 @@ def test_table_shards_assemble(rm, gpu, R0):
     got = np.zeros_like(full)
     for s in range(N):
         for lr in range(cap.value):
-            g = rm.lib().rm_shard_row(H, R, R0, s, N, lr)
+            g = rm.lib().rm_shard_to_global(H, R, R0, N, s, lr)
             if g >= 0:
                 got[g] = parts[s][lr]
     np.testing.assert_array_equal(got, full)

@@ -87,7 +87,7 @@ def test_weighted_default_is_plain_interleave(rm):
         for s in range(N):
             a = rm.shard_global_rows(H, R, s, N)
             assert (a == rm.shard_global_rows(H, R, s, N, R)).all()
-            assert [rm.lib().rm_shard_global_row(H, R, s, N, r) for r in range(len(a))] == a.tolist()
+            assert [rm.lib().rm_shard_to_global(H, R, 0, N, s, r) for r in range(len(a))] == a.tolist()
 
 
 def test_weighted_rank0_share_at_4k(rm):
@@ -117,7 +117,8 @@ def test_weighted_schedule_rejects_bad_maps(rm):
     assert L.rm_shard_rows(64, 0, 8, 2, 0, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
     assert L.rm_shard_rows(64, 8, 8, 2, 2, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
     assert L.rm_shard_rows(64, 1 << 29, 8, 4, 0, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
-    assert L.rm_shard_row(64, 8, 7, 3, 2, 0) == -1
+    assert L.rm_shard_to_global(64, 8, 7, 2, 3, 0) == -1  # shard 3 of 2
+    assert L.rm_shard_to_global(64, 8, 7, 2, 1, -1) == -1
     assert L.rm_shard_owner(64, 8, 7, 2, 64, C.byref(n), C.byref(cap)) == rm.RM_ERR_INVALID
 
 

@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
   rm_ctx* c;
   if (rm_create(&c, &cfg)) return 1;
   int rows = H;
-  rm_shard_rows_cap(H, 8, nsh, &rows);
+  rm_shard_rows(H, 8, 0, nsh, 0, nullptr, &rows);
   if (nsh <= 1) rows = H;
   const size_t nw = (size_t)(W / 4) * ((rows + 3) / 4);
   unsigned long long* d;
