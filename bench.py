@@ -227,9 +227,12 @@ def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int
     0.0124 / 0.0594 for 10 on 2 (round 4, tools/probe_batch.py --steps 120,
     profiles/r04_probe_batch120.txt); fewer steps cap the batch so that the launches
     still spread over the 3 contexts.  The 4K supersampled frames fill the chip by
-    themselves: pairs of frames on 4 contexts measure 0.8 % faster than single frames
-    on 3 (0.8193 against 0.8258 ms, 7 interleaved rounds, profiles/r04_inflight.txt);
-    the 8K graph-replayed frames (cfg5) stay single, 3 in flight.
+    themselves: single frames on 3 contexts (k_sample) measure 1.4 % (cfg3) and 1.3 %
+    (cfg4) faster than pairs on 4 (k_sample_frames: the same VALU instructions per
+    frame, 7 % more SALU) since round 5's kernel (round 6, tools/ab_issue.sh, 5
+    interleaved rounds: 0.7041 against 0.7139 ms, profiles/r06_ab_issue.txt; round 4
+    had measured pairs 0.8 % ahead); the 8K graph-replayed frames (cfg5) stay single,
+    3 in flight.
 
     N > 1: pairs of frames per launch on 2 contexts (round 6, tools/probe_scale.py,
     profiles/r06_scale.txt): a rank's 1/N share of a frame is shorter than its
@@ -243,7 +246,7 @@ def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int
         return 2
     if config in (1, 2):
         return max(1, min(20, -(-steps // 3)))
-    return 2 if config in (3, 4) else 1
+    return 1
 
 
 def _gather_objects(mine, ws):
@@ -362,8 +365,7 @@ def main() -> int:
                     help="frames in flight: consecutive frames render from separate contexts on "
                          "separate streams, so frame f+1's waves fill the SIMDs that frame f's "
                          "last long waves leave idle (1 = one context, frames in turn; "
-                         "0 = 3 on one GPU (4 for the 4K pairs), 2 on a sharded frame, each "
-                         "launch two frames)")
+                         "0 = 3 on one GPU, 2 on a sharded frame, each launch two frames)")
     ap.add_argument("--batch", type=int, default=-1,
                     help="frames per launch (rm_dispatch_frames: one grid over B frames, so frame "
                          "k+1's waves fill the SIMDs frame k's longest waves leave idle); 1 = one "
@@ -443,7 +445,7 @@ def main() -> int:
         batch = 1  # a graph replays one frame
     # contexts in flight: 3 frames or batches on one GPU (4 for the 4K pairs), 2
     # batches of a sharded step (default_batch)
-    nfl = args.inflight if args.inflight > 0 else (2 if sharded else (4 if batch == 2 and args.config in (3, 4) else 3))
+    nfl = args.inflight if args.inflight > 0 else (2 if sharded else 3)
     nfl = nfl if (not sharded or args.pipeline) else 1
     if one_comm:
         nfl = 1  # one context, one communicator; batches overlap through its gather stream

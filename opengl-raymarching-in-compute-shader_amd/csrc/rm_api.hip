@@ -1754,7 +1754,14 @@ int graph_frame(rm_ctx* c) {
       (rc = graph_capture(c, F)) != RM_OK)
     return rc;
   rm_graph_slot& g = c->gs;
+  // a specialised table's render node is its batch kernel with one frame
+  // (rm_jit.hpp launch_table_jit): its argument is a FrameBatch
+  static thread_local rmd::FrameBatch GB;
   void* args[] = {&F};
+  if (c->graph_jit) {
+    GB.f[0] = F;
+    args[0] = &GB;
+  }
   hipKernelNodeParams kp;
   RM_HIP(c, hipGraphKernelNodeGetParams(g.render, &kp));
   kp.kernelParams = args;

@@ -51,10 +51,16 @@ namespace {
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, rm::JitTable*> g_cache;
 
-// [aa][counters] as JitTable::fn, then the batch kernels [aa] (JitTable::fnb)
-const char* const kNames[3][2] = {{"rmd::k_table_pixel<false>", "rmd::k_table_pixel<true>"},
-                                  {"rmd::k_table_sample<false>", "rmd::k_table_sample<true>"},
+// The counting kernels [aa] (JitTable::fnc), then the production batch kernels
+// [aa] (JitTable::fnb).  A specialised table renders every production frame with
+// the batch kernel, a single frame as a batch of one (round 6):
+// the single-frame production kernel, whose whole Frame lives in SGPRs from the
+// prologue on, spilled two VGPRs at the 8-wave bound (12 B of scratch per lane,
+// 1.19x the image's HBM bytes) where the batch kernel, reading its frame at a
+// run-time offset of the argument block, needs none.
+const char* const kNames[2][2] = {{"rmd::k_table_pixel<true>", "rmd::k_table_sample<true>"},
                                   {"rmd::k_table_pixel_frames<>", "rmd::k_table_sample_frames<>"}};
+constexpr int kProd[2] = {2, 3};  // the production kernels' indices in `lowered`
 }  // namespace
 
 namespace rm {
@@ -174,15 +180,14 @@ int jit_compile_waves(const uint32_t* words, int32_t n, const std::string& arch,
   return RM_OK;
 }
 
-// Waves per SIMD the production kernels (k_table_*<false>, lowered[0] and [2],
-// and the batch kernels, [4] and [5]) of a compiled code object run at, or 0
-// when any needs scratch;
+// Waves per SIMD the production kernels (the batch kernels, kProd) of a
+// compiled code object run at, or 0 when any needs scratch;
 // -1 (with err) when a descriptor is missing: that is an error, not a spill, as
 // silently falling back to the generic kernel would hide a code-object layout
 // change.
 int production_waves(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
   int w = 8;
-  for (int k : {0, 2, 4, 5}) {
+  for (int k : kProd) {
     long priv = -1;
     int vg = 0;
     if (!kernel_desc(c, l[k], &priv, &vg)) {
@@ -200,7 +205,7 @@ int production_waves(const std::vector<char>& c, const std::vector<std::string>&
 // err) when a descriptor is missing.
 long production_scratch(const std::vector<char>& c, const std::vector<std::string>& l, std::string& err) {
   long most = 0;
-  for (int k : {0, 2, 4, 5}) {
+  for (int k : kProd) {
     long priv = -1;
     int vg = 0;
     if (!kernel_desc(c, l[k], &priv, &vg)) {
@@ -313,10 +318,10 @@ int jit_table(const uint32_t* words, int32_t n, const JitTable** out, std::strin
     return RM_OK;
   }
   hipError_t e = hipModuleLoadData(&j->mod, code.data());
-  for (int k = 0; k < 4 && e == hipSuccess; ++k)
-    e = hipModuleGetFunction(&j->fn[k / 2][k % 2], j->mod, lowered[k].c_str());
   for (int k = 0; k < 2 && e == hipSuccess; ++k)
-    e = hipModuleGetFunction(&j->fnb[k], j->mod, lowered[4 + k].c_str());
+    e = hipModuleGetFunction(&j->fnc[k], j->mod, lowered[k].c_str());
+  for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    e = hipModuleGetFunction(&j->fnb[k], j->mod, lowered[kProd[k]].c_str());
   if (e != hipSuccess) {
     if (j->mod) (void)hipModuleUnload(j->mod);
     delete j;
@@ -329,12 +334,16 @@ int jit_table(const uint32_t* words, int32_t n, const JitTable** out, std::strin
 }
 
 hipError_t launch_table_jit(const JitTable* j, const rmd::Frame& F, bool counters, hipStream_t s) {
+  if (!counters) {
+    // production: the batch kernel over a batch of one (kNames)
+    static thread_local rmd::FrameBatch B;
+    B.f[0] = F;
+    return launch_table_jit_frames(j, B, 1, s);
+  }
   void* args[] = {const_cast<rmd::Frame*>(&F)};
   if (F.aa)
-    return hipModuleLaunchKernel(j->fn[1][counters], (F.width + 3) / 4, (F.rows + 3) / 4, 1, 64, 1, 1, 0, s,
-                                 args, nullptr);
-  return hipModuleLaunchKernel(j->fn[0][counters], (F.width + 7) / 8, (F.rows + 7) / 8, 1, 64, 1, 1, 0, s, args,
-                               nullptr);
+    return hipModuleLaunchKernel(j->fnc[1], (F.width + 3) / 4, (F.rows + 3) / 4, 1, 64, 1, 1, 0, s, args, nullptr);
+  return hipModuleLaunchKernel(j->fnc[0], (F.width + 7) / 8, (F.rows + 7) / 8, 1, 64, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t launch_table_jit_frames(const JitTable* j, const rmd::FrameBatch& B, int n, hipStream_t s) {

@@ -22,9 +22,10 @@ def test_default_batches():
     assert b.default_batch(2, False, False, 120) == 20
     assert b.default_batch(2, False, False, 20) == 7
     assert b.default_batch(1, False, False, 1) == 1
-    # cfg3 / cfg4: pairs; cfg5 (graph-replayed 8K frames): single frames
-    assert b.default_batch(3, False, False, 30) == 2
-    assert b.default_batch(4, False, False, 20) == 2
+    # cfg3 / cfg4: single frames since round 6 (tools/ab_issue.sh); cfg5 (graph-
+    # replayed 8K frames): single frames
+    assert b.default_batch(3, False, False, 30) == 1
+    assert b.default_batch(4, False, False, 20) == 1
     assert b.default_batch(5, False, False, 20) == 1
     # N > 1: pairs of frames per launch (round 6, tools/probe_scale.py), or batches
     # of 4 on one communicator
