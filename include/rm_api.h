@@ -219,7 +219,10 @@ int rm_dispatch(rm_ctx *ctx);
  * scene table's frames batch the same way (API version 5; its specialised
  * kernels too).  Frames with a different AA setting, or (specialised tables) a
  * camera that needs the generic kernel, render in separate launches.  Not
- * available with cfg.counters. */
+ * available with cfg.counters.  Every frame's uniforms are checked before any
+ * launch; a batch that still fails (a HIP or RCCL error part way) leaves the
+ * context's uniforms as before the call, and its image and ring hold
+ * undefined contents until the next successful dispatch. */
 #define RM_MAX_BATCH 32
 int rm_dispatch_frames(rm_ctx *ctx, const rm_uniforms *frames, int32_t n);
 /* Wait for all work queued on the context (== glMemoryBarrier + the

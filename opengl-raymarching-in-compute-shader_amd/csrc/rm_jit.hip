@@ -249,6 +249,16 @@ int jit_compile(const uint32_t* words, int32_t n, const std::string& arch, std::
   if (rc != RM_OK) return rc;
   const long sc = production_scratch(c, l, err);
   if (sc < 0) return RM_ERR_HIP;
+  if (const char* lg = std::getenv("RM_JIT_LOG"); lg && *lg == '1') {
+    //  which kernels set the bound: the production batch kernels,
+    // which render single frames too (kNames)
+    for (int k : kProd) {
+      long priv = 0;
+      int vg = 0;
+      if (kernel_desc(c, l[k], &priv, &vg))
+        std::fprintf(stderr, "rm_jit:   8-wave bound: %s %d VGPRs, %ld B scratch\n", l[k].c_str(), vg, priv);
+    }
+  }
   if (sc <= kFewSpillBytes) {
     code.swap(c);
     lowered.swap(l);

@@ -178,6 +178,9 @@ def test_table_compiles_once(rm, tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [x for x in out.stderr.splitlines() if x.startswith("rm_jit: hiprtc compile")]
     assert len(lines) == 1, out.stderr
+    #  the log names the kernels that set the bound: the batch kernels
+    bound = [x for x in out.stderr.splitlines() if x.startswith("rm_jit:   8-wave bound")]
+    assert len(bound) == 2 and all("_frames" in x and " 0 B scratch" in x for x in bound), out.stderr
     rc, co = _code_object(rm, rm.default_scene())
     assert rc == 0
     vg = _kernel_vgprs(co)
