@@ -74,13 +74,13 @@ CONFIGS = {
 }
 SWEEP_FRAMES = 120
 
-# Rank 0 also assembles every gathered frame (k_unshard, HBM-bound: 2 x the RGBA8
-# image at ~6.4 TB/s).  Its time over one GPU's render time of the whole frame, per
-# config, measured on one MI355X (tools/probe_unshard.py, profiles/r05_unshard.txt;
-# frame times of DESIGN §9): --rank0-share -1 gives rank 0 the rows per round that
-# balance its render + assembly against the other ranks' render
-# (rm.best_rank0_rows).
-ASSEMBLE_RATIO = {1: 0.57, 2: 0.079, 3: 0.0145, 4: 0.0134, 5: 0.0158}  # round 5 frame times
+# Rank 0 also assembles every gathered frame (k_unshard, HBM-bound: the RGB8 shards
+# read and the RGBA8 frame written at ~6.3 TB/s).  Its time over one GPU's render
+# time of the whole frame, per config, measured on one MI355X (tools/probe_unshard.py,
+# profiles/r06_unshard_rgb8.txt: 3.6 / 3.8 / 9.3 / 9.3 / 36.0 us; frame times of
+# DESIGN §9): --rank0-share -1 gives rank 0 the rows per round that balance its
+# render + assembly against the other ranks' render (rm.best_rank0_rows).
+ASSEMBLE_RATIO = {1: 0.58, 2: 0.082, 3: 0.0132, 4: 0.0122, 5: 0.0139}  # round 6
 
 
 def bench_frames(steps: int) -> list:

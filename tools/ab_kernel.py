@@ -43,7 +43,10 @@ def child_batch(cfg, frames, B, nctx):
 
     def run():
         for j, i in enumerate(range(0, frames, B)):
-            rs[j % nctx].dispatch_frames(us[i:i + B])
+            if B == 1:  # single frames through rm_dispatch (k_sample / k_pixel), as bench.py
+                rs[j % nctx].dispatch(us[i])
+            else:
+                rs[j % nctx].dispatch_frames(us[i:i + B])
         for r in rs:
             r.synchronize()
     t_end = time.perf_counter() + 0.3

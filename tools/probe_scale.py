@@ -52,7 +52,7 @@ STREAMS = os.environ.get("PROBE_STREAMS", "hip")
 FMT = os.environ.get("PROBE_FMT", "rgb8")
 
 W, H, B3, AA, SH = CFGS[CFG]
-ASSEMBLE_RATIO = {2: 0.079, 3: 0.0145, 4: 0.0134, 5: 0.0158}
+ASSEMBLE_RATIO = {2: 0.082, 3: 0.0132, 4: 0.0122, 5: 0.0139}  # bench.py
 frames = [(k * 120 // K) % 120 for k in range(K)]
 U = {f: rm.sweep_uniforms(f, 120, B3, AA, SH) for f in set(frames)}
 
