@@ -218,7 +218,7 @@ def comm_ids(n: int, rank: int) -> list:
     return ids
 
 
-def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int:
+def default_batch(config: int, sharded: bool, one_comm: bool, steps: int, table: bool = False) -> int:
     """Frames per launch when --batch is not given (measured).
 
     One GPU: cfg1 / cfg2 frames (4K / 32K one-wave workgroups) are shorter than their
@@ -232,7 +232,9 @@ def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int
     frame, 7 % more SALU) since round 5's kernel (round 6, tools/ab_issue.sh, 5
     interleaved rounds: 0.7041 against 0.7139 ms, profiles/r06_ab_issue.txt; round 4
     had measured pairs 0.8 % ahead); the 8K graph-replayed frames (cfg5) stay single,
-    3 in flight.
+    3 in flight.  A runtime scene table's 4K frames keep pairs on 4 contexts: its
+    kernels gain from them (generic -2.5 %, specialised -0.7 % per cfg3 frame against
+    single frames on 3, profiles/r06_ab_tables.txt).
 
     N > 1: pairs of frames per launch on 2 contexts (round 6, tools/probe_scale.py,
     profiles/r06_scale.txt): a rank's 1/N share of a frame is shorter than its
@@ -246,7 +248,7 @@ def default_batch(config: int, sharded: bool, one_comm: bool, steps: int) -> int
         return 2
     if config in (1, 2):
         return max(1, min(20, -(-steps // 3)))
-    return 1
+    return 2 if table and config in (3, 4) else 1
 
 
 def _gather_objects(mine, ws):
@@ -439,13 +441,15 @@ def main() -> int:
     # stream, image and (N > 1) RCCL communicator, so frame f+1's waves fill the SIMDs
     # that frame f's last long waves leave idle, and frame f gathers while f+1 renders.
     one_comm = sharded and args.comms == 1
-    batch = args.batch if args.batch > 0 else default_batch(args.config, sharded, one_comm, args.steps)
+    batch = (args.batch if args.batch > 0
+             else default_batch(args.config, sharded, one_comm, args.steps, args.scene != "builtin"))
     batch = max(1, min(batch, rm.RM_MAX_BATCH, args.steps))
     if use_graph:
         batch = 1  # a graph replays one frame
     # contexts in flight: 3 frames or batches on one GPU (4 for the 4K pairs), 2
     # batches of a sharded step (default_batch)
-    nfl = args.inflight if args.inflight > 0 else (2 if sharded else 3)
+    nfl = args.inflight if args.inflight > 0 else (2 if sharded else (4 if batch == 2 and args.config in (3, 4)
+                                                                    else 3))
     nfl = nfl if (not sharded or args.pipeline) else 1
     if one_comm:
         nfl = 1  # one context, one communicator; batches overlap through its gather stream

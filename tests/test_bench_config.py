@@ -26,6 +26,8 @@ def test_default_batches():
     # replayed 8K frames): single frames
     assert b.default_batch(3, False, False, 30) == 1
     assert b.default_batch(4, False, False, 20) == 1
+    # a scene table's 4K frames keep pairs (profiles/r06_ab_tables.txt)
+    assert b.default_batch(3, False, False, 20, table=True) == 2
     assert b.default_batch(5, False, False, 20) == 1
     # N > 1: pairs of frames per launch (round 6, tools/probe_scale.py), or batches
     # of 4 on one communicator
