@@ -62,6 +62,8 @@ struct TCnt {
 // compile-time flags of the march-loop variants (no <type_traits> under hiprtc)
 struct Yes { static constexpr bool value = true; };
 struct No { static constexpr bool value = false; };
+template <int V>
+struct IntC { static constexpr int value = V; };
 
 using rm::TABLE_WORDS;
 
@@ -165,6 +167,10 @@ struct Table {
   int fpswz;
   const float* sb;  // the lazy slots' balls, 4 words each (centre, radius), slot order, in LDS
   bool fpaxis;  // normal (0, n_y, 0): the plane is q.y n_y + w (the specialised kernel's shortcut)
+  // ... with centre y 0 and n_y = 1, unswizzled (the reference's floor): q.y = p.y - 0 = p.y and
+  // q.y * 1 = q.y exactly for every float, so the plane is the one add p.y + w (round 6: the
+  // specialised kernel folds the same at compile time)
+  bool fpunit;
 #endif
   float blend, omblend;
 
@@ -174,6 +180,7 @@ struct Table {
     // q.x n_x and q.z n_z are signed zeros for finite q: the sum is q.y n_y + w
     // (prim_dist's RM_TABLE_STATIC shortcut, here on a uniform flag: -1.2 % per
     // cfg3 frame; the per-lane test inside the type switch had measured +5 %)
+    if (fpunit) return p.y + fpw;
     if (fpaxis) return ((fpswz == RM_SWIZZLE_XZY ? p.z - fpc[2] : p.y - fpc[1])) * fpn[1] + fpw;
     f3 q = sub(p, mk(fpc[0], fpc[1], fpc[2]));
     if (fpswz == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
@@ -248,9 +255,20 @@ struct Table {
     const float* ex = exits();
     const float p1 = (fabsf(pos.x) + fabsf(pos.y)) + fabsf(pos.z);
     float U = INF;
+#ifndef RM_TABLE_STATIC
+    // the planes' bound from the fast plane, or the plane mask: no pass over every
+    // entry's type (round 6: -1 % per cfg3 frame, profiles/r06_ab_gen3.txt)
+    if (fp >= 0) {
+      U = gmin(U, plane_fast(pos));  // (TLazy::dist's bound the same way)
+    } else {
+      for (uint32_t pm = __float_as_uint(ex[rm::EX_PLANE_MASK]); pm; pm &= pm - 1u)
+        U = gmin(U, prim_dist(entry(__builtin_ctz(pm)), RM_PRIM_PLANE, pos, blend, omblend));
+    }
+#else
     RM_TS_UNROLL
     for (int k = 0; k < n; ++k)
       if (type(k) == RM_PRIM_PLANE) U = gmin(U, prim_dist(entry(k), RM_PRIM_PLANE, pos, blend, omblend));
+#endif
     const float e = 0.001f + 0x1p-22f * (p1 + 1.0f);
     const float Ue = U + ((1.0f + ex[rm::EX_LIP]) * e * (1.0f + 0x1p-10f) + 0x1p-20f * fabsf(U));
     const float slack = ex[rm::EX_SIGMA] * ((p1 + 0.002f) + ex[rm::EX_S]) *
@@ -268,6 +286,42 @@ struct Table {
       }
       if (wany(!cull)) keep |= 1u << k;
     }
+#ifndef RM_TABLE_STATIC
+    // The generic kernel (round 6): the kept entries in table order, each entry's
+    // words read from LDS once and its type switched on once for all four samples
+    // (one sample at a time, every sample had re-read the entry and re-run the
+    // switch): -8.4 % per cfg3 frame (profiles/r06_ab_gen2.txt; the words moved to
+    // scalar registers instead, v_readfirstlane each, gave -4.0 %).  Per sample the
+    // same opU over the same entries in the same order: the same four values.
+    float d0 = INF, dx = INF, dy = INF, dz = INF;
+    for (uint32_t w = keep; w; w &= w - 1u) {
+      const int k = __builtin_ctz(w);
+      float P[TABLE_WORDS];
+#pragma unroll
+      for (int i = rm::TW_SWIZZLE; i < rm::TW_BALL; ++i) P[i] = entry(k)[i];
+      auto eval4 = [&](auto T) {
+        constexpr int ty = decltype(T)::value;
+        auto opu = [](float d, float v) { return d < v ? d : v; };
+        if (!have_c0) d0 = opu(d0, prim_dist<kBoundedPoints>(P, ty, pos, blend, omblend));
+        dx = opu(dx, prim_dist<kBoundedPoints>(P, ty, px, blend, omblend));
+        dy = opu(dy, prim_dist<kBoundedPoints>(P, ty, py, blend, omblend));
+        dz = opu(dz, prim_dist<kBoundedPoints>(P, ty, pz, blend, omblend));
+      };
+      switch (type(k)) {
+        case RM_PRIM_SPHERE: eval4(IntC<RM_PRIM_SPHERE>()); break;
+        case RM_PRIM_BOX: eval4(IntC<RM_PRIM_BOX>()); break;
+        case RM_PRIM_BLEND: eval4(IntC<RM_PRIM_BLEND>()); break;
+        case RM_PRIM_TORUS: eval4(IntC<RM_PRIM_TORUS>()); break;
+        case RM_PRIM_CAPSULE: eval4(IntC<RM_PRIM_CAPSULE>()); break;
+        default: eval4(IntC<RM_PRIM_PLANE>()); break;
+      }
+    }
+    if (!have_c0) c0 = d0;
+    vx = dx;
+    vy = dy;
+    vz = dz;
+    return;
+#endif
     // one sample at a time (fewer live values): opU in table order over `keep`
     // (an entry this lane culled is strictly above its minimum at the sample)
     auto sample = [&](f3 q) {
@@ -706,7 +760,13 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
       #pragma unroll
       for (int j = 0; j < KL; ++j) {
         if (j >= ns || !wany(tt >= lz.te[j])) continue;
-#ifdef RM_TABLE_STATIC  // (the specialised kernels: the type is known at compile time)
+        // (a compile-time test in the specialised kernels; a uniform branch in the
+        // generic one's 5-slot instance since round 6: -1 % per cfg3 frame,
+        // profiles/r06_ab_gen2.txt; in the 8-slot instance it makes the batch kernel
+        // copy its FrameBatch argument to scratch, 12 KB per lane)
+#ifndef RM_TABLE_STATIC
+        if (KL <= rm::TABLE_FEW_SLOTS)
+#endif
         if (S.type(j) == RM_PRIM_TORUS) {
           // evaluated instead of re-tested, as the built-in march does (rm_scene.hpp
           // scene_lazy): the exact value is the budget's lower bound
@@ -716,7 +776,6 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
           lz.te[j] = vmax(__builtin_fmaf(v - pl, lz.invp, tt), lz.te[j]);
           continue;
         }
-#endif
 #ifdef RM_TABLE_STATIC
         const float* B = S.entry(j) + rm::TW_BALL;
 #else
@@ -1216,6 +1275,9 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
     S.fpw = uword(P + rm::TW_P + 3);
     S.fpswz = __float_as_int(uword(P + rm::TW_SWIZZLE));
     S.fpaxis = S.fpn[0] == 0.0f && S.fpn[2] == 0.0f;
+    // (+0 exactly: p.y - (+0) = p.y for every p.y, -0 included; a -0 centre would turn
+    // p.y = -0 into +0)
+    S.fpunit = S.fpaxis && S.fpswz != RM_SWIZZLE_XZY && __float_as_uint(S.fpc[1]) == 0u && S.fpn[1] == 1.0f;
   }
   return S;
 #endif
