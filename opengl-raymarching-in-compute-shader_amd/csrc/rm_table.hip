@@ -379,11 +379,11 @@ struct Table {
   __device__ __forceinline__ int id(int k) const { return __float_as_int(entry(k)[rm::TW_ID]); }
   // True when no step of a march from ro along rd can see a distance > tmax:
   // some axis-aligned plane (normal (0, n_y, 0), a specialised table's
-  // compile-time test) has a value that does not grow along the ray and starts
-  // at or below tmax.  Its float value RN(RN(q.y n_y) + off), q.y = RN(p.y - c.y),
+  // compile-time test, the generic kernel's fast plane) has a value that does not
+  // grow along the ray and starts at or below tmax.  Its float value RN(RN(q.y n_y) + off), q.y = RN(p.y - c.y),
   // p.y = RN(ro.y + RN(rd.y t)), is monotone in t (rounding is monotone), non-
   // increasing when n_y rd.y <= 0, and the minimum is at most that value.  NaNs
-  // fail every compare (false).  The generic kernel proves nothing (false).
+  // fail every compare (false).
   __device__ __forceinline__ bool no_escape(f3 ro, f3 rd, float tmax) const {
     bool ok = false;
 #ifdef RM_TABLE_STATIC
@@ -397,6 +397,16 @@ struct Table {
       const float cy = swz ? P[rm::TW_CENTER + 2] : P[rm::TW_CENTER + 1];
       const bool mono = (a[1] > 0.0f && ry <= 0.0f) || (a[1] < 0.0f && ry >= 0.0f);
       ok = ok || (mono && (oy - cy) * a[1] + a[3] <= tmax);
+    }
+#else
+    // the generic kernel's fast plane when axis-aligned: the same argument with
+    // its staged parameters (round 6: the escape compare leaves the step loop of
+    // waves of downward rays, -1.5 % per cfg3 frame, profiles/r06_ab_gen5.txt)
+    if (fp >= 0 && fpaxis) {
+      const bool swz = fpswz == RM_SWIZZLE_XZY;
+      const float oy = swz ? ro.z : ro.y, ry = swz ? rd.z : rd.y, cy = swz ? fpc[2] : fpc[1];
+      const bool mono = (fpn[1] > 0.0f && ry <= 0.0f) || (fpn[1] < 0.0f && ry >= 0.0f);
+      ok = mono && (oy - cy) * fpn[1] + fpw <= tmax;
     }
 #endif
     return ok;
