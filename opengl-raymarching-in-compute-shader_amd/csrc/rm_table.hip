@@ -823,7 +823,9 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
     t = tp;
   };
   const bool useT = wany(!(T == __builtin_huge_valf()));
-  if (__all(S.no_escape(ro, rd, tmax))) {
+  // (the generic 8-slot instance keeps its escape compare: the proof's registers
+  // spilled it, 12 B of scratch per lane)
+  if ((kBoundedPoints || KL <= rm::TABLE_FEW_SLOTS) && __all(S.no_escape(ro, rd, tmax))) {
     if (useT) run(No(), Yes());
     else run(No(), No());
   } else {
