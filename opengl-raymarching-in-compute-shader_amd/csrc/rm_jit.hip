@@ -11,10 +11,11 @@
 //
 // Register bound per table.  First compile: bounded to 8 waves per SIMD, kept
 // when the production kernels spill at most kFewSpillBytes of scratch per lane
-// (their kernel descriptors' private segment).  The reference scene's kernels
-// spill 7 VGPRs there (32 B) and render a cfg3 frame 1.8 % faster than at the
-// spill-free 7-wave bound (round 4, profiles/r04_spec_waves.txt); a table whose
-// kernels fit 64 registers compiles the same as without a bound.  Otherwise the
+// (their kernel descriptors' private segment).  The reference scene's batch
+// kernels need none there (round 6); in round 4 its single-frame kernels spilled
+// 7 VGPRs (32 B) and still rendered a cfg3 frame 1.8 % faster than at the
+// spill-free 7-wave bound (profiles/r04_spec_waves.txt), hence the allowance.  A
+// table whose kernels fit 64 registers compiles the same as without a bound.  Otherwise the
 // spill-free ladder: a compile without an occupancy bound (RM_TABLE_MIN_WAVES =
 // 1), whose descriptors give each production kernel's VGPR allocation (a kernel
 // allocating at most 512 / w registers runs at w waves with no scratch), and
