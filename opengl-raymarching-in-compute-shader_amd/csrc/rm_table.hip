@@ -810,6 +810,21 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   };
   float tp = t;
   auto run = [&](auto esc, auto useT) {
+    if (!decltype(esc)::value && !decltype(useT)::value) {
+      // downward waves: t advances at the top of the step and the loop carries
+      // only the step's (t, d) (the built-in march's form, rm_kernels.hip; round
+      // 6: generic -0.5 %, specialised -0.4 % per cfg3 frame,
+      // profiles/r06_ab_thadd_*.txt)
+      float dp = 0.0f;
+      for (int i = i0;; ++i) {
+        t = t + dp;
+        const float d = step(t);
+        dp = d;
+        if ((d < 0.000001f * t) | (i >= nmax)) break;
+      }
+      dl = dp;
+      return;
+    }
     for (int i = i0;; ++i) {
       const float d = step(t);
       bool e = d < 0.000001f * t;
@@ -975,6 +990,17 @@ __device__ __forceinline__ THit gmarch(const Table& S, f3 ro, f3 rd, bool reflec
   };
   float tp = t;
   auto run = [&](auto esc, auto useT) {
+    if (!decltype(esc)::value && !decltype(useT)::value) {  // (smarch's form)
+      float dp = 0.0f;
+      for (int i = i0;; ++i) {
+        t = t + dp;
+        const float d = step(t);
+        dp = d;
+        if ((d < 0.000001f * t) | (i >= nmax)) break;
+      }
+      dl = dp;
+      return;
+    }
     for (int i = i0;; ++i) {
       const float d = step(t);
       bool e = d < 0.000001f * t;

@@ -38,7 +38,10 @@ enum Kind { FMA = 0, ADD = 1, SQRT = 2, MIX = 3, DEP = 4, ADDMUL = 5, FMAADD = 6
             A_MUL = 8, A_MIN = 9, A_MIN3 = 10, A_MOV = 11, A_CND = 12, A_CMP = 13, A_U32 = 14, A_E64 = 15,
             // operand sources: VGPR, SGPR, literal, inline constant
             O_VV = 16, O_VS = 17, O_VL = 18, O_VI = 19, O_FMAVVV = 20, O_FMAVSV = 21, O_FMAC = 22,
-            O_MULL = 23, O_MAXVV = 24, O_CNDS = 25, O_SUB = 26, O_CMPS = 27, O_FMAVVL = 28 };
+            O_MULL = 23, O_MAXVV = 24, O_CNDS = 25, O_SUB = 26, O_CMPS = 27, O_FMAVVL = 28,
+            // integer min / max and bit operations on float bit patterns (round 6)
+            I_MINI = 29, I_MAXI = 30, I_MINU = 31, I_MAXU = 32, I_AND = 33, I_OR = 34, I_MAX3I = 35,
+            I_MED3 = 36, I_PKADD = 37 };
 
 template <int K>
 __global__ __launch_bounds__(64, 8) void k_issue(float* out, unsigned long long* clk, float s) {
@@ -81,6 +84,18 @@ __global__ __launch_bounds__(64, 8) void k_issue(float* out, unsigned long long*
       if (K == O_CMPS) asm volatile("v_cmp_lt_f32_e64 s[2:3], %0, %1" : : "v"(a[j]), "v"(b) : "s2", "s3");
       if (K == O_FMAVVL) asm volatile("v_fmamk_f32 %0, %0, 0x3f7ff000, %1" : "+v"(a[j]) : "v"(b));
       if (K == A_E64) asm volatile("v_add_f32_e64 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_MINI) asm volatile("v_min_i32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_MAXI) asm volatile("v_max_i32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_MINU) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_MAXU) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_AND) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_OR) asm volatile("v_or_b32 %0, %0, %1" : "+v"(a[j]) : "v"(b));
+      if (K == I_MAX3I) asm volatile("v_max3_i32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+      if (K == I_MED3) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+      if (K == I_PKADD && (j & 1) == 0) {
+        // one v_pk_add_f32 per two accumulators (a wave64 packed op covers both)
+        asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(*reinterpret_cast<double*>(&a[j])) : "v"(*reinterpret_cast<const double*>(&a[(j + 2) % kAcc])));
+      }
     }
   }
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
@@ -131,7 +146,7 @@ void run(const char* name, int nblk, float* out, unsigned long long* clk) {
   CK(hipEventDestroy(e1));
 }
 
-int main() {
+int main(int argc, char**) {
   hipDeviceProp_t p;
   CK(hipGetDeviceProperties(&p, 0));
   const int nblk = p.multiProcessorCount * 4 * 8;  // 8 one-wave workgroups per SIMD
@@ -142,6 +157,20 @@ int main() {
   unsigned long long* clk;
   CK(hipMalloc(&out, sizeof(float) * 64 * nblk));
   CK(hipMalloc(&clk, sizeof(unsigned long long) * nblk));
+  if (argc > 1) {  // the round-6 kinds only
+    run<I_MINI>("min.i32", nblk, out, clk);
+    run<I_MAXI>("max.i32", nblk, out, clk);
+    run<I_MINU>("min.u32", nblk, out, clk);
+    run<I_MAXU>("max.u32", nblk, out, clk);
+    run<I_AND>("and.b32", nblk, out, clk);
+    run<I_OR>("or.b32", nblk, out, clk);
+    run<I_MAX3I>("max3.i32", nblk, out, clk);
+    run<I_MED3>("med3.f32", nblk, out, clk);
+    run<I_PKADD>("pkadd(x2)", nblk, out, clk);
+    run<O_MAXVV>("max.vv", nblk, out, clk);
+    run<A_U32>("u32", nblk, out, clk);
+    return 0;
+  }
   run<FMA>("fma", nblk, out, clk);
   run<ADD>("add", nblk, out, clk);
   run<SQRT>("sqrt", nblk, out, clk);
