@@ -1483,22 +1483,26 @@ namespace rm {
 
 namespace {
 template <int KL, int SL>
+void launch_table_frames_kl(const rmd::FrameBatch& B, int n, hipStream_t s);
+// A production frame renders with the batch kernel, as a batch of one (round 6,
+// as the specialised kernels: rm_jit.hip): the single-frame production kernel,
+// whose Frame lives in scalar registers from the prologue on, was 1.0 % slower
+// per cfg3 frame (profiles/r06_ab_b1_single.txt) and is no longer compiled.  The
+// counting kernels keep their single-frame form.
+template <int KL, int SL>
 void launch_table_kl(const rmd::Frame& F, bool counters, hipStream_t s) {
+  if (!counters) {
+    static thread_local rmd::FrameBatch B;
+    B.f[0] = F;
+    launch_table_frames_kl<KL, SL>(B, 1, s);
+    return;
+  }
   // the table, then the lazy slots' balls (Table::sb)
   const size_t lds = (((rm::scene_words(F.nprims) + 3) & ~(size_t)3) + 4 * (size_t)rm::EX_MAX_SLOTS) * sizeof(float);
-  if (F.aa) {
-    const dim3 g((F.width + 3) / 4, (F.rows + 3) / 4);
-    if (counters)
-      hipLaunchKernelGGL((rmd::k_table_sample<true, KL>), g, dim3(64), lds, s, F);
-    else
-      hipLaunchKernelGGL((rmd::k_table_sample<false, KL, SL>), g, dim3(64), lds, s, F);
-  } else {
-    const dim3 g((F.width + 7) / 8, (F.rows + 7) / 8);
-    if (counters)
-      hipLaunchKernelGGL((rmd::k_table_pixel<true, KL>), g, dim3(64), lds, s, F);
-    else
-      hipLaunchKernelGGL((rmd::k_table_pixel<false, KL, SL>), g, dim3(64), lds, s, F);
-  }
+  if (F.aa)
+    hipLaunchKernelGGL((rmd::k_table_sample<true, KL>), dim3((F.width + 3) / 4, (F.rows + 3) / 4), dim3(64), lds, s, F);
+  else
+    hipLaunchKernelGGL((rmd::k_table_pixel<true, KL>), dim3((F.width + 7) / 8, (F.rows + 7) / 8), dim3(64), lds, s, F);
 }
 
 template <int KL, int SL>

@@ -38,16 +38,16 @@ def test_diagnostic_build_compiles(name, tmp_path):
 BUILD = os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd", "build")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 # Scratch bytes per lane each production kernel may use: none for the built-in
-# kernels; the generic table kernel's instances none, or 8-12 B in the 8-slot
-# reference-shaped one (round 6: 12 B in its single-frame kernel since the normals'
-# plane bound comes from the fast plane, -1 % on the reference scene; round 5: the
-# output index re-formed after the march and the expiries' first values formed
-# where each march starts; round 4: 28-32 B, and 588 B once after a change to its
-# bounce loop).
+# kernels; the generic table kernel's batch kernels (every production frame since
+# round 6, a single one as a batch of one) none, or 8 B in the 8-slot instances
+# (round 5: the output index re-formed after the march and the expiries' first
+# values formed where each march starts; round 4: 28-32 B, and 588 B once after a
+# change to its bounce loop).  The single-frame table kernels are counting kernels
+# only (k_table_*<true, KL>).
 # (keys: substrings of the mangled names -- k_pixel<false>, k_sample<false>, the
-# batched k_*_frames, k_table_*<false, KL> and their batches)
+# batched k_*_frames and the table batch kernels k_table_*_frames<KL, SL>)
 SCRATCH_MAX = {"7k_pixelILb0E": 0, "8k_sampleILb0E": 0, "14k_pixel_frames": 0,
-               "15k_sample_frames": 0, "13k_table_pixelILb0E": 8, "14k_table_sampleILb0E": 12,
+               "15k_sample_frames": 0, "20k_table_pixel_framesILi5E": 0, "21k_table_sample_framesILi5E": 0,
                "20k_table_pixel_frames": 8, "21k_table_sample_frames": 8}
 
 
@@ -67,6 +67,8 @@ def test_production_kernels_scratch(obj, tmp_path):
     cos = [p for p in os.listdir(tmp_path) if "gfx950" in p]
     assert len(cos) == 1, os.listdir(tmp_path)
     priv = _kernel_private_sizes(open(tmp_path / cos[0], "rb").read())
+    if obj == "rm_table.o":  # production frames are batches (of one): no single-frame production kernels
+        assert not any("k_table_sampleILb0E" in k or "k_table_pixelILb0E" in k for k in priv), priv
     seen = 0
     for sym, size in priv.items():
         for key, cap in SCRATCH_MAX.items():

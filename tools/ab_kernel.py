@@ -31,7 +31,23 @@ CFGS = {1: (512, 512, 0, False, 1), 2: (1920, 1080, 1, False, 0), 3: (3840, 2160
         4: (3840, 2160, 5, True, 0), 5: (7680, 4320, 3, True, 0)}
 
 
-def child_batch(cfg, frames, B, nctx):
+def table_scene(rm):
+    """The reference scene as a runtime table (RM_AB_WIDE=1: two more spheres
+    before its floor, 7 bounded entries: the tables' 8-slot instances)."""
+    sc = rm.default_scene()
+    if os.environ.get("RM_AB_WIDE") == "1":
+        import ctypes as C
+        extra = []
+        for dx in (40.0, -40.0):
+            q = rm.rm_primitive()
+            C.memmove(C.byref(q), C.byref(sc[0]), C.sizeof(q))
+            q.center[0] += dx
+            extra.append(q)
+        sc = sc[:-1] + extra + sc[-1:]
+    return sc
+
+
+def child_batch(cfg, frames, B, nctx, table=False, spec=False):
     import time
     sys.path.insert(0, os.environ.get("RM_PKG_DIR") or os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd"))
     import torch  # noqa: F401
@@ -40,6 +56,11 @@ def child_batch(cfg, frames, B, nctx):
     W, H, b, aa, sm = CFGS[cfg]
     us = [rm.sweep_uniforms((k * 120) // frames, 120, b, aa, sm) for k in range(frames)]
     rs = [rm.Renderer(W, H) for _ in range(nctx)]
+    for r in rs:
+        if spec:
+            r.specialize_scene(True)
+        if table or spec:
+            r.set_scene(table_scene(rm))
 
     def run():
         for j, i in enumerate(range(0, frames, B)):
@@ -70,18 +91,7 @@ def child(cfg, frames, table, spec=False):
         if spec:
             r.specialize_scene(True)
         if table or spec:
-            sc = rm.default_scene()
-            if os.environ.get("RM_AB_WIDE") == "1":
-                # 7 bounded entries and the floor last: the 8-slot instances
-                import ctypes as C
-                extra = []
-                for dx in (40.0, -40.0):
-                    q = rm.rm_primitive()
-                    C.memmove(C.byref(q), C.byref(sc[0]), C.sizeof(q))
-                    q.center[0] += dx
-                    extra.append(q)
-                sc = sc[:-1] + extra + sc[-1:]
-            r.set_scene(sc)
+            r.set_scene(table_scene(rm))
         r.enable_timing(True)
         for f in range(3):
             r.dispatch(rm.sweep_uniforms(f, 120, b, aa, sm))
@@ -106,7 +116,7 @@ def main():
     a = ap.parse_args()
     if a.child:
         if a.batch:
-            return child_batch(a.cfg, a.frames, a.batch, a.ctx)
+            return child_batch(a.cfg, a.frames, a.batch, a.ctx, a.table, a.spec)
         return child(a.cfg, a.frames, a.table, a.spec)
     libs = a.libs or ([os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd/librm.so")]
                       + sorted(p for p in glob.glob(os.path.join(ROOT, "tools/variants/librm_*.so"))

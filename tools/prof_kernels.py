@@ -29,10 +29,10 @@ with rm.Renderer(cfg["width"], cfg["height"], kernel=k) as r:
     if kname in ("table", "table-spec"):  # the reference scene as a runtime table (k_table_* kernels)
         r.set_scene(rm.default_scene())
     us = [rm.sweep_uniforms(f, 120, cfg["bounces"], cfg["aa"], cfg["shadow"]) for f in bench_frames(steps)]
-    # (a specialised table renders single frames with its batch kernel too, as a
-    # batch of one: with BATCH > 1 only the batches run, so the batch kernel's
-    # per-launch counters are all launches of BATCH frames)
-    if not (kname == "table-spec" and batch > 1):
+    # (a table renders single frames with its batch kernel too, as a batch of
+    # one: with BATCH > 1 only the batches run, so the batch kernel's per-launch
+    # counters are all launches of BATCH frames)
+    if not (kname in ("table", "table-spec") and batch > 1):
         for u in us:
             r.dispatch(u)
     r.synchronize()
