@@ -151,6 +151,10 @@ __device__ __forceinline__ float prim_dist(const float* P, int type, f3 p, float
   }
 }
 
+// The slots' balls are staged with their radius negated (Table::sb), so the
+// re-test's fma(|p - c|, 1 - 2^-12, -R) takes it as a VGPR addend with its
+// literal factor (v_fmamk_f32, dual-issued) instead of the factor in an SGPR.
+#define RM_SBR(r) (-(r))
 struct Table {
   const float* t;  // LDS (or global) copy of the compiled table
 #ifdef RM_TABLE_STATIC
@@ -165,7 +169,7 @@ struct Table {
   int fp;
   float fpc[3], fpn[3], fpw;
   int fpswz;
-  const float* sb;  // the lazy slots' balls, 4 words each (centre, radius), slot order, in LDS
+  const float* sb;  // the lazy slots' balls, 4 words each (centre, -radius: RM_SBR), slot order, in LDS
   bool fpaxis;  // normal (0, n_y, 0): the plane is q.y n_y + w (the specialised kernel's shortcut)
   // ... with centre y 0 and n_y = 1, unswizzled (the reference's floor): q.y = p.y - 0 = p.y and
   // q.y * 1 = q.y exactly for every float, so the plane is the one add p.y + w (round 6: the
@@ -591,7 +595,7 @@ struct TLazy {
           // the slot's ball gathered at staging: one 16-byte LDS read (-0.9 / -1.9 %
           // per cfg3 / cfg2 frame against its four words read through the entry)
           const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];
-          const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+          const float B[4] = {B4.x, B4.y, B4.z, RM_SBR(B4.w)};
 #else
           const float* B = S.entry(k) + rm::TW_BALL;
 #endif
@@ -723,7 +727,16 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
   const float* PL = S.entry(kp);
   auto plane = [&](float y) { return prim_dist(PL, RM_PRIM_PLANE, mk(0.0f, y, 0.0f), S.blend, S.omblend); };
 #else
-  auto plane = [&](float y) { return S.plane_fast(mk(0.0f, y, 0.0f)); };
+  // the reference's floor (fpunit) as the common path, p.y + w with w in a VGPR
+  // (an SGPR operand takes a whole issue slot), other planes overwrite it (round 6:
+  // -0.5 % per cfg3 frame, -1.5 % cfg2; the step's value no longer needs a copy
+  // to merge two paths, profiles/r06_ab_tnu*.txt)
+  const float pw = topaque(S.fpw);
+  auto plane = [&](float y) {
+    float m = y + pw;
+    if (!S.fpunit) m = S.plane_fast(mk(0.0f, y, 0.0f));
+    return m;
+  };
 #endif
   SLazy<KL> lz;
   {
@@ -790,7 +803,7 @@ __device__ __forceinline__ THit smarch(const Table& S, f3 ro, f3 rd, bool reflec
         const float* B = S.entry(j) + rm::TW_BALL;
 #else
         const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];  // the slot's ball, staged
-        const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+        const float B[4] = {B4.x, B4.y, B4.z, RM_SBR(B4.w)};
 #endif
         const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
@@ -963,7 +976,7 @@ __device__ __forceinline__ THit gmarch(const Table& S, f3 ro, f3 rd, bool reflec
         const float* B = S.entry((int)ex[rm::EX_SLOTS + j]) + rm::TW_BALL;
 #else
         const float4 B4 = reinterpret_cast<const float4*>(S.sb)[j];  // the slot's ball, staged
-        const float B[4] = {B4.x, B4.y, B4.z, B4.w};
+        const float B[4] = {B4.x, B4.y, B4.z, RM_SBR(B4.w)};
 #endif
         const float bx = p.x - B[0], by = p.y - B[1], bz = p.z - B[2];
         const float lb = __builtin_fmaf(__builtin_amdgcn_sqrtf((bx * bx + by * by) + bz * bz),
@@ -1298,7 +1311,10 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
     const int nw = (int)rm::scene_words(F.nprims);
     float* sb = lds + ((nw + 3) & ~3);
     const int l = threadIdx.x, ns = (int)S.exits()[rm::EX_NSLOTS];
-    if (l < 4 * ns) sb[l] = S.entry((int)S.exits()[rm::EX_SLOTS + l / 4])[rm::TW_BALL + l % 4];
+    if (l < 4 * ns) {
+      const float v = S.entry((int)S.exits()[rm::EX_SLOTS + l / 4])[rm::TW_BALL + l % 4];
+      sb[l] = l % 4 == 3 ? RM_SBR(v) : v;
+    }
     __syncthreads();
     S.sb = sb;
   }
