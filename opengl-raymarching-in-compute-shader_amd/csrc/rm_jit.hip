@@ -224,8 +224,15 @@ constexpr long kFewSpillBytes = 32;  // 8 spilled VGPRs per lane
 // fits no bound (the reference scene's objects repeated, on the build host's
 // CPU: 12 entries 26 s, one compile that fits 8 waves; 16 entries 261 s for the
 // 8-wave compile alone, 3.7 MB of code, and 786 s for the ladder, which ends
-// on the generic kernel).  They render with the generic kernel at once.
-constexpr int32_t kJitMaxEntries = 12;
+// on the generic kernel; round 6, with the single-frame production kernels no
+// longer compiled: 12 entries 22 s, 16 entries 509 s for the ladder, still ending
+// on the generic kernel: 88 VGPRs and 400 B of scratch at 8 waves, spills at 6).
+// They render with the generic kernel at once.  RM_JIT_MAX_ENTRIES (a build
+// define) moves the cap for such measurements.
+#ifndef RM_JIT_MAX_ENTRIES
+#define RM_JIT_MAX_ENTRIES 12
+#endif
+constexpr int32_t kJitMaxEntries = RM_JIT_MAX_ENTRIES;
 
 // The table kernels at their register bound (above): *waves is the waves per
 // SIMD they run at, or 0 (code left empty) when no bound fits.
