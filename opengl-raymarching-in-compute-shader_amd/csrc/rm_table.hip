@@ -162,13 +162,21 @@ struct Table {
 #else
   int n;
   // The fast plane (generic kernel): the table's only plane when it has exactly
-  // one (the reference's floor, and most scenes), with its parameters in scalar
-  // registers from staging on, so the every-step plane evaluation needs no LDS
-  // reads, no type dispatch and no entry loop (plane_fast: prim_dist's plane
-  // arithmetic, the same float operations).  fp = -1: none.
+  // one (the reference's floor, and most scenes), staged so that the every-step
+  // plane evaluation needs no type dispatch and no entry loop (plane_fast:
+  // prim_dist's plane arithmetic, the same float operations); the reference's
+  // floor (fpunit) is one add of the offset w.  fp = -1: none.
   int fp;
-  float fpc[3], fpn[3], fpw;
-  int fpswz;
+  // The fast plane's offset w in a scalar register; its centre, normal and
+  // swizzle are read from its LDS entry where a path needs them (round 6: held in
+  // scalar registers they took 7 of the kernel's, which is at its scalar-register
+  // limit: 13 -> 2 spilled SGPRs and no scratch in the reference-shaped instance,
+  // -0.7 % per cfg3 frame; the tilted-plane shape, whose every step reads them,
+  // +5 %; profiles/r06_ab_fplds*.txt)
+  float fpw;
+  __device__ __forceinline__ float FPC(int j) const { return t[fp * TABLE_WORDS + rm::TW_CENTER + j]; }
+  __device__ __forceinline__ float FPN(int j) const { return t[fp * TABLE_WORDS + rm::TW_P + j]; }
+  __device__ __forceinline__ int FPSWZ() const { return __float_as_int(t[fp * TABLE_WORDS + rm::TW_SWIZZLE]); }
   const float* sb;  // the lazy slots' balls, 4 words each (centre, -radius: RM_SBR), slot order, in LDS
   bool fpaxis;  // normal (0, n_y, 0): the plane is q.y n_y + w (the specialised kernel's shortcut)
   // ... with centre y 0 and n_y = 1, unswizzled (the reference's floor): q.y = p.y - 0 = p.y and
@@ -185,10 +193,10 @@ struct Table {
     // (prim_dist's RM_TABLE_STATIC shortcut, here on a uniform flag: -1.2 % per
     // cfg3 frame; the per-lane test inside the type switch had measured +5 %)
     if (fpunit) return p.y + fpw;
-    if (fpaxis) return ((fpswz == RM_SWIZZLE_XZY ? p.z - fpc[2] : p.y - fpc[1])) * fpn[1] + fpw;
-    f3 q = sub(p, mk(fpc[0], fpc[1], fpc[2]));
-    if (fpswz == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
-    return dot(q, mk(fpn[0], fpn[1], fpn[2])) + fpw;
+    if (fpaxis) return ((FPSWZ() == RM_SWIZZLE_XZY ? p.z - FPC(2) : p.y - FPC(1))) * FPN(1) + fpw;
+    f3 q = sub(p, mk(FPC(0), FPC(1), FPC(2)));
+    if (FPSWZ() == RM_SWIZZLE_XZY) q = mk(q.x, q.z, q.y);
+    return dot(q, mk(FPN(0), FPN(1), FPN(2))) + fpw;
   }
 #endif
 
@@ -407,10 +415,10 @@ struct Table {
     // its staged parameters (round 6: the escape compare leaves the step loop of
     // waves of downward rays, -1.5 % per cfg3 frame, profiles/r06_ab_gen5.txt)
     if (fp >= 0 && fpaxis) {
-      const bool swz = fpswz == RM_SWIZZLE_XZY;
-      const float oy = swz ? ro.z : ro.y, ry = swz ? rd.z : rd.y, cy = swz ? fpc[2] : fpc[1];
-      const bool mono = (fpn[1] > 0.0f && ry <= 0.0f) || (fpn[1] < 0.0f && ry >= 0.0f);
-      ok = mono && (oy - cy) * fpn[1] + fpw <= tmax;
+      const bool swz = FPSWZ() == RM_SWIZZLE_XZY;
+      const float oy = swz ? ro.z : ro.y, ry = swz ? rd.z : rd.y, cy = swz ? FPC(2) : FPC(1);
+      const bool mono = (FPN(1) > 0.0f && ry <= 0.0f) || (FPN(1) < 0.0f && ry >= 0.0f);
+      ok = mono && (oy - cy) * FPN(1) + fpw <= tmax;
     }
 #endif
     return ok;
@@ -1322,16 +1330,17 @@ __device__ __forceinline__ Table stage(const Frame& F, float* lds) {
   S.fp = (pm != 0 && (pm & (pm - 1u)) == 0) ? __builtin_ctz(pm) : -1;
   if (S.fp >= 0) {
     const float* P = S.entry(S.fp);
+    float c[3], nv[3];
     for (int j = 0; j < 3; ++j) {
-      S.fpc[j] = uword(P + rm::TW_CENTER + j);
-      S.fpn[j] = uword(P + rm::TW_P + j);
+      c[j] = uword(P + rm::TW_CENTER + j);
+      nv[j] = uword(P + rm::TW_P + j);
     }
+    const int swz = __float_as_int(uword(P + rm::TW_SWIZZLE));
     S.fpw = uword(P + rm::TW_P + 3);
-    S.fpswz = __float_as_int(uword(P + rm::TW_SWIZZLE));
-    S.fpaxis = S.fpn[0] == 0.0f && S.fpn[2] == 0.0f;
+    S.fpaxis = nv[0] == 0.0f && nv[2] == 0.0f;
     // (+0 exactly: p.y - (+0) = p.y for every p.y, -0 included; a -0 centre would turn
     // p.y = -0 into +0)
-    S.fpunit = S.fpaxis && S.fpswz != RM_SWIZZLE_XZY && __float_as_uint(S.fpc[1]) == 0u && S.fpn[1] == 1.0f;
+    S.fpunit = S.fpaxis && swz != RM_SWIZZLE_XZY && __float_as_uint(c[1]) == 0u && nv[1] == 1.0f;
   }
   return S;
 #endif

@@ -39,17 +39,17 @@ BUILD = os.path.join(ROOT, "opengl-raymarching-in-compute-shader_amd", "build")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 # Scratch bytes per lane each production kernel may use: none for the built-in
 # kernels; the generic table kernel's batch kernels (every production frame since
-# round 6, a single one as a batch of one) 8-12 B in the supersampled ones and the
-# 8-slot instances (round 6: one VGPR spilled since the reference's floor became
-# the step's common path, -0.5 % per cfg3 frame; round 5: the output index
+# round 6, a single one as a batch of one) none in the 5-slot instances, 8 B in
+# some 8-slot ones (round 6: the fast plane's centre and normal moved from scalar
+# registers to LDS took the reference-shaped kernel's last spill; round 5: the output index
 # re-formed after the march and the expiries' first values formed where each march
 # starts; round 4: 28-32 B, and 588 B once after a change to its bounce loop).
 # The single-frame table kernels are counting kernels only (k_table_*<true, KL>).
 # (keys: substrings of the mangled names -- k_pixel<false>, k_sample<false>, the
 # batched k_*_frames and the table batch kernels k_table_*_frames<KL, SL>)
 SCRATCH_MAX = {"7k_pixelILb0E": 0, "8k_sampleILb0E": 0, "14k_pixel_frames": 0,
-               "15k_sample_frames": 0, "20k_table_pixel_framesILi5E": 0,
-               "20k_table_pixel_frames": 8, "21k_table_sample_frames": 12}
+               "15k_sample_frames": 0, "20k_table_pixel_framesILi5E": 0, "21k_table_sample_framesILi5E": 0,
+               "20k_table_pixel_frames": 8, "21k_table_sample_frames": 8}
 
 
 @pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not installed")
