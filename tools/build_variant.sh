@@ -3,6 +3,7 @@
 #   tools/build_variant.sh NAME [-DFOO=1 ...]   -> tools/variants/librm_NAME.so
 #   tools/build_variant.sh NAME --rev GITREV    -> librm built from a committed revision
 #   tools/build_variant.sh NAME --patch F.diff  -> librm built with a patch applied
+#   KOPT=-O3 tools/build_variant.sh NAME         -> the built-in kernels at another -O level
 #                                                 (experiments live as patches, not knobs)
 set -e
 name=$1; shift
@@ -28,8 +29,8 @@ b=$(mktemp -d)
 case "$*" in
   *RM_STATS*) /opt/rocm/bin/hipcc $flags -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" & ;;
   *) pslp=-fno-slp-vectorize; [ -n "$RM_PIXEL_SLP" ] && pslp=-fslp-vectorize
-     /opt/rocm/bin/hipcc $flags -O2 $pslp -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
-     /opt/rocm/bin/hipcc $flags -O2 -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels_aa.o" & ;;
+     /opt/rocm/bin/hipcc $flags ${KOPT:--O2} $pslp -DRM_KERNELS_PIXEL_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels.o" &
+     /opt/rocm/bin/hipcc $flags ${KOPT:--O2} -fno-slp-vectorize -DRM_KERNELS_AA_ONLY -c "$src/$pkg/csrc/rm_kernels.hip" -o "$b/rm_kernels_aa.o" & ;;
 esac
 /opt/rocm/bin/hipcc $flags -x c++ -c "$src/$pkg/csrc/rm_host.cpp" -o "$b/rm_host.o" &
 [ -f "$src/$pkg/csrc/rm_comm.cpp" ] && { /opt/rocm/bin/hipcc $flags -x hip -c "$src/$pkg/csrc/rm_comm.cpp" -o "$b/rm_comm.o" & }
