@@ -125,6 +125,11 @@ def pmc_entry(kernel_name: str, workload: str):
         stem = kernel_name[:-1] if kernel_name.endswith(">") else kernel_name
         for k, v in d.items():
             if (kernel_name in k or stem + "," in k) and "hbm_bytes_per_launch" in v:
+                # a batch kernel's counters are per frame only when the summary divided
+                # them by the frames of a launch (tools/summarize_profiles.py records
+                # frames_per_launch); an entry without it is per launch: not used
+                if "_frames" in k and "frames_per_launch" not in v:
+                    continue
                 return v, os.path.basename(path)
     return None, None
 

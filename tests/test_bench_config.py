@@ -62,3 +62,17 @@ def test_gpus_beyond_the_visible_devices_exits_2():
     assert out.returncode == 2, (out.returncode, out.stderr[-2000:])
     assert "--gpus 64 in one process needs 64 visible devices" in out.stderr
     assert out.stdout.strip() == ""
+
+
+def test_committed_pmc_entries_are_per_frame():
+    """The roofline reads per-frame PMC values from profiles/ (bench.pmc_entry): every batch
+    kernel it would use carries the frames per launch its summary divided by (the batched
+    configurations' launches of 20 and 2 frames), and the single-frame kernels none."""
+    b = _bench()
+    for kernel, workload, frames in (("k_pixel_frames", "cfg1", 20), ("k_pixel_frames", "cfg2", 20),
+                                     ("k_table_sample_frames", "cfg3", 2),
+                                     ("k_table_sample_frames", "cfg3-spec", 2),
+                                     ("k_sample<false>", "cfg3", None), ("k_sample<false>", "cfg4", None)):
+        v, src = b.pmc_entry(kernel, workload)
+        assert v is not None, (kernel, workload)
+        assert v.get("frames_per_launch") == frames, (kernel, workload, src, v.get("frames_per_launch"))
